@@ -1,0 +1,263 @@
+"""Benchmark: CDS bases extracted + translated per second on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
+    torchrun --nproc-per-node N bench.py --gpus N ...        (one rank per GPU)
+
+A step is one launch of the fused gather + reverse-complement + translate
+kernel over the rank's whole resident workload (packed genome and interval
+tables already in HBM; nucleotide and peptide outputs written to HBM).
+Workload (BASELINE.json configs[2]): a 1 Gb synthetic
+genome, 500k multi-exon transcripts (1+Poisson(7) exons, U[50,250] bases,
+both strands), outputs nucleotide + peptide.  Multi-GPU is weak scaling: the
+N-rank job is an N Gb genome sharded by contig, each rank owning a C3-shaped
+shard (seed + rank); transcripts never span shards, so there is no
+data-path collective.  torch.distributed is used for the barrier and the
+max-over-ranks timing only.
+
+Rank 0 prints ONE JSON line (contract in README/DESIGN.md).
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+
+
+def log(msg):
+    if int(os.environ.get('RANK', '0')) == 0:
+        sys.stderr.write('[bench] %s\n' % msg)
+        sys.stderr.flush()
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world == 1:
+        return None, rank, local, world
+    import torch
+    import torch.distributed as dist
+    backend = 'gloo'
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        backend = 'nccl'            # RCCL on ROCm
+    dist.init_process_group(backend=backend)
+    return dist, rank, local, world
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def allreduce_max(dist, x):
+    if dist is None:
+        return x
+    import torch
+    dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allreduce_sum(dist, x):
+    if dist is None:
+        return x
+    import torch
+    dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's per-record loop (CPU oracle restatement of
+# genome.py:603-822), single core, on a bounded sample of the same workload.
+# ---------------------------------------------------------------------------
+
+def cpu_baseline(w, budget_bases):
+    from oracle import magot_oracle as mo
+    step = max(1, int(w.cds_bases // max(budget_bases, 1)))
+    tx_ids = np.arange(0, w.n_tx, step)
+    aset = mo.OracleSet()
+    used = sorted(set(w.tx_contig[tx_ids].tolist()))
+    seqs = {w.contig_names[c]: w.contig_bytes(c).tobytes().decode('latin-1') for c in used}
+    aset.genome = mo.OracleGenome(seqs)
+    aset.mRNA = {}
+    first = np.concatenate([[0], np.cumsum(w.ex_count)])
+    recs = []
+    bases = 0
+    for t in tx_ids.tolist():
+        sid = w.contig_names[w.tx_contig[t]]
+        st = '-' if w.tx_strand[t] < 0 else '+'
+        kids = []
+        for e in range(first[t], first[t + 1]):
+            cid = 'cds%d_%d' % (t, e)
+            c0 = int(w.ex_start[e]) + 1
+            c1 = int(w.ex_start[e] + w.ex_len[e])
+            aset.CDS[cid] = mo.OBase(cid, sid, (c0, c1), 'CDS', 'rna%d' % t, st, {}, aset)
+            kids.append(cid)
+            bases += int(w.ex_len[e])
+        rna = mo.OParent('rna%d' % t, sid, 'mRNA', kids, None, st, aset, {})
+        aset.mRNA[rna.ID] = rna
+        recs.append(rna)
+    t0 = time.perf_counter()
+    for r in recs:
+        mo.get_fasta(r, aset, 'nucleotide')
+    t1 = time.perf_counter()
+    for r in recs:
+        mo.get_fasta(r, aset, 'protein')
+    t2 = time.perf_counter()
+    return {'value': bases / (t2 - t0), 'unit': 'bases/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d of %d transcripts (every %d-th), %d CDS bases; get_fasta nucleotide '
+                      '%.2fs + protein %.2fs; pure-Python restatement of the reference loop '
+                      '(oracle/magot_oracle.py)' % (len(recs), w.n_tx, step, bases, t1 - t0,
+                                                   t2 - t1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', default='C3', choices=['C2', 'C3', 'C5'])
+    ap.add_argument('--no-verify', action='store_true', help='skip the oracle byte check')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-sample-bases', type=float, default=5.0e7)
+    ap.add_argument('--pmc-json', default=os.path.join(ROOT, 'profiles', 'pmc_C3.json'),
+                    help='per-launch HBM traffic measured with rocprofv3 --pmc')
+    args = ap.parse_args()
+
+    dist, rank, local, world = dist_setup(args.gpus)
+    os.environ.setdefault('MAGOT_DEVICE', str(local))
+
+    from magot_amd import _lib, engine, synth
+
+    t0 = time.perf_counter()
+    seed = synth.SEED_BASE + {'C2': 2, 'C3': 3, 'C5': 5}[args.config] + 1000 * rank
+    w = synth.make(args.config, seed=seed)
+    t_gen = time.perf_counter() - t0
+    log('generated %s shard: %d contigs, %d transcripts, %d exons, %d CDS bases (%.1fs)'
+        % (args.config, len(w.contig_len), w.n_tx, w.n_exons, w.cds_bases, t_gen))
+
+    ctx = _lib.Context(local)
+    t0 = time.perf_counter()
+    dev = engine.DeviceGenome(w.contigs(), ctx=ctx)
+    t_pack = time.perf_counter() - t0
+    ex, tx = w.plan_tables()
+    outputs = engine.OUT_NUC | (engine.OUT_PEP if w.outputs == 'nuc+pep' else 0)
+    t0 = time.perf_counter()
+    plan = engine.ExtractionPlan(dev, ex, tx, outputs)
+    t_plan = time.perf_counter() - t0
+    B, P = plan.nuc_bytes, plan.pep_bytes
+    alg_bytes = plan.algorithmic_bytes
+
+    # -- correctness of the measured configuration --------------------------
+    parity = 'not checked'
+    t_fetch = None
+    if not args.no_verify:
+        t0 = time.perf_counter()
+        nuc, noff, pep, poff = plan.run()
+        t_fetch = time.perf_counter() - t0
+        from oracle import cds_oracle
+        ref, roff, st = cds_oracle.extract_workload(w, False)
+        ok = (not st.any()) and np.array_equal(nuc, ref) and \
+            np.array_equal(noff.astype(np.int64), roff)
+        if ok and pep is not None:
+            pref, proff, pst = cds_oracle.extract_workload(w, True)
+            starts = poff[:-1].astype(np.int64)
+            lens = (poff[1:] - poff[:-1]).astype(np.int64)
+            first = np.zeros(len(starts), dtype=bool)
+            first[lens > 0] = pep[starts[lens > 0]] == ord('X')
+            keep = np.ones(len(pep), dtype=bool)
+            keep[starts[first]] = False
+            ok = np.array_equal(pep[keep], pref)
+        del nuc, pep
+        parity = 'bit-exact vs CPU oracle (full output)' if ok else 'MISMATCH'
+        if not ok:
+            log('PARITY FAILURE on rank %d' % rank)
+    ok_all = allreduce_sum(dist, 0.0 if parity.startswith('bit-exact') or args.no_verify else 1.0)
+
+    # -- timed region ---------------------------------------------------------
+    for _ in range(args.warmup):
+        plan.execute()
+    ctx.sync()
+    barrier(dist)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute()
+    ctx.sync()
+    elapsed = time.perf_counter() - t0
+    barrier(dist)
+    elapsed_max = allreduce_max(dist, elapsed)
+
+    # per-launch kernel duration from HIP events on the context stream
+    kernel_ms = plan.time(max(5, min(args.steps, 20)))
+    kernel_ms_max = allreduce_max(dist, kernel_ms)
+    total_bases = allreduce_sum(dist, float(B))
+
+    value = total_bases * args.steps / elapsed_max
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        with open(args.pmc_json) as fh:
+            pmc = json.load(fh)
+        if pmc.get('config') == args.config:
+            traffic = pmc.get('hbm_bytes_per_launch')
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log('timing the CPU baseline on a bounded sample ...')
+        cpu = cpu_baseline(w, args.cpu_sample_bases)
+
+    if rank == 0:
+        desc = {'C3': '1 Gb genome (64 lognormal contigs) + 500k transcripts x (1+Poisson(7)) '
+                      'exons of U[50,250] b, both strands; nucleotide + peptide out',
+                'C2': '100 Mb genome, 50k single-exon + CDS U[150,1850]; nucleotide out',
+                'C5': '3 Gb genome, 2M transcripts; nucleotide + peptide out'}[args.config]
+        rec = {
+            'metric': 'CDS bases extracted+translated/sec',
+            'value': value,
+            'unit': 'bases/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': elapsed_max / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'u8',
+            'data': 'synthetic (seeded, SURVEY.md 8(d))',
+            'config': {'workload': '%s per rank: %s' % (args.config, desc),
+                       'cds_bases_per_rank': B, 'residues_per_rank': P,
+                       'exons_per_rank': int(w.n_exons), 'transcripts_per_rank': int(w.n_tx),
+                       'parallelism': 'contig-sharded x%d (weak)' % world},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
+                         'kernel': 'extract_kernel', 'kernel_ms': kernel_ms,
+                         'kernel_ms_max_rank': kernel_ms_max,
+                         'algorithmic_bytes_per_launch': alg_bytes},
+            'cpu_baseline': cpu,
+            'parity': parity if ok_all == 0 else 'MISMATCH on %d rank(s)' % int(ok_all),
+            'phases_s': {'generate': t_gen, 'pack_h2d': t_pack, 'plan_h2d': t_plan,
+                         'execute_fetch_d2h': t_fetch},
+        }
+        print(json.dumps(rec), flush=True)
+    plan.close()
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

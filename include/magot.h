@@ -1,0 +1,176 @@
+/*
+ * magot.h -- C ABI of libmagot.so, the MI355X (gfx950) extraction engine behind
+ * the magot_amd Python package.
+ *
+ * The reference (Huangtianyu-caas/MAGOT, Python 2.7) has no FFI: its hot path is
+ * the pure-Python call chain
+ *     AnnotationSet.get_fasta          genome.py:578-582
+ *       ParentAnnotation.get_fasta     genome.py:677-731
+ *         BaseAnnotation.get_seq       genome.py:603-614
+ *           Sequence.reverse_compliment genome.py:784-793
+ *         Sequence.translate           genome.py:795-822
+ * over a GenomeSequence dict (genome.py:854-877).  This header is the boundary
+ * that chain is cut at: the Python layer (magot_amd/genome.py) walks the
+ * annotation graph exactly as the reference does and hands the resulting
+ * interval lists to this library; every byte of sequence output is produced
+ * by HIP kernels.  Plain pointers and sizes only -- no torch types.
+ *
+ * Ownership: callers own every host buffer; the library owns device memory
+ * behind the opaque handles, released by the matching *_destroy.
+ * Errors: every int-returning call returns MAGOT_OK (0) or a negative status;
+ * magot_last_error() gives a thread-local message.
+ * Threading: a magot_ctx is bound to one device and one HIP stream and is not
+ * thread-safe; use one context per host thread.  One process per GPU.
+ */
+#ifndef MAGOT_H
+#define MAGOT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MAGOT_ABI_VERSION 1
+
+enum magot_status {
+  MAGOT_OK = 0,
+  MAGOT_ERR_ARG = -1,      /* bad argument / inconsistent tables           */
+  MAGOT_ERR_HIP = -2,      /* HIP runtime failure (no device, OOM, fault)   */
+  MAGOT_ERR_RANGE = -3,    /* interval outside its contig                   */
+  MAGOT_ERR_STATE = -4     /* call out of order (e.g. fetch before execute) */
+};
+
+/* Output selection for a plan (magot_plan_create.outputs). */
+#define MAGOT_OUT_NUC 1u   /* spliced CDS nucleotides  (seq_type="nucleotide") */
+#define MAGOT_OUT_PEP 2u   /* frame-0 translation      (seq_type="protein")    */
+
+/*
+ * One interval of one record, already in OUTPUT order.
+ *   start_rc : bits 0..62 = 0-based start inside the contig (the Python slice
+ *              contig[c0-1:c1] already normalised by slice.indices, so
+ *              genome.py:606/608 semantics incl. clamping are resolved);
+ *              bit 63 = reverse-complement this interval (strand '-',
+ *              genome.py:607-608).
+ *   contig   : index into the contig list given to magot_genome_load.
+ *   len      : number of bases (0 allowed: empty Python slice).
+ * Replaces: BaseAnnotation.get_seq (genome.py:603-614) per child, ordered as
+ * ParentAnnotation.get_fasta orders them (genome.py:689-703).
+ */
+typedef struct magot_exon {
+  uint64_t start_rc;
+  uint32_t contig;
+  uint32_t len;
+} magot_exon;
+
+/*
+ * One output record = the contiguous exon range [exon_begin, exon_begin+n_exons).
+ * Records must tile the exon table in order (exon_begin[t+1] ==
+ * exon_begin[t] + n_exons[t]).  flags is reserved (0).
+ * Replaces: the "".join of genome.py:702-705 for one ParentAnnotation.
+ */
+typedef struct magot_tx {
+  uint64_t exon_begin;
+  uint32_t n_exons;
+  uint32_t flags;
+} magot_tx;
+
+typedef struct magot_ctx magot_ctx;
+typedef struct magot_genome magot_genome;
+typedef struct magot_plan magot_plan;
+
+/* ABI version compiled into the library (== MAGOT_ABI_VERSION). */
+int magot_abi_version(void);
+
+/* Thread-local text of the last failure on this thread ("" if none). */
+const char* magot_last_error(void);
+
+/* Number of visible HIP devices (0 when none / runtime unavailable). */
+int magot_device_count(void);
+
+/* Bind a context to HIP device `device` with a private non-blocking stream. */
+int magot_ctx_create(int device, magot_ctx** out);
+void magot_ctx_destroy(magot_ctx* ctx);
+
+/*
+ * Pack a genome into HBM: 2-bit codes (ACGT, case-folded), a 1-bit soft-mask
+ * plane, and a run list of every other byte (N, IUPAC, '-', spaces ...) with a
+ * 4096-base directory.  seqs[i] points at lens[i] raw bytes of contig i,
+ * exactly the bytes genome.py:875 keeps (every byte except CR/LF).
+ * Replaces: GenomeSequence (genome.py:854-877) as the data the path reads.
+ */
+int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
+                      uint32_t n_contigs, magot_genome** out);
+/* Sizes of a loaded genome: total bases, exception runs, device bytes held. */
+int magot_genome_stats(const magot_genome* g, uint64_t* total_bases, uint64_t* n_exc_runs,
+                       uint64_t* device_bytes);
+void magot_genome_destroy(magot_genome* g);
+
+/*
+ * Build a device-resident plan: interval table -> output offsets, 12 KiB
+ * output tiles, per-tile exon and record ranges, all uploaded to HBM.
+ * nuc_bytes / pep_bytes receive the total output sizes (pep_bytes counts the
+ * untrimmed frame-0 translation, floor(len/3) per record; the single leading
+ * 'X' trim of genome.py:819-821 is applied by the caller on fetch).
+ */
+int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* exons,
+                      uint64_t n_exons, const magot_tx* txs, uint64_t n_tx, uint32_t outputs,
+                      magot_plan** out, uint64_t* nuc_bytes, uint64_t* pep_bytes);
+void magot_plan_destroy(magot_plan* p);
+
+/* Enqueue the fused gather + reverse-complement + translate kernel on the
+ * context stream (asynchronous; outputs stay in HBM). */
+int magot_plan_execute(magot_ctx* ctx, magot_plan* p);
+
+/* Block until the context stream is idle. */
+int magot_ctx_sync(magot_ctx* ctx);
+
+/* Copy outputs to caller buffers (synchronous).  Any pointer may be NULL to
+ * skip it.  nuc_off / pep_off receive n_tx+1 prefix offsets. */
+int magot_plan_fetch(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off,
+                     uint8_t* pep_out, uint64_t* pep_off);
+
+/* execute + sync + fetch. */
+int magot_run(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off,
+              uint8_t* pep_out, uint64_t* pep_off);
+
+/*
+ * Kernel timing: execute `iters` times back to back on the context stream with
+ * HIP events around each launch; *avg_ms receives the mean launch duration.
+ */
+int magot_plan_time(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms);
+
+/* Device-resident output pointers of a plan (for on-device consumers/tests). */
+int magot_plan_device_outputs(magot_plan* p, void** nuc_dev, void** pep_dev);
+
+/* Algorithmic byte count per execute of a plan (the roofline numerator):
+ * ceil(B/4) + B*[nuc] + P*[pep] + 16*E + 32*T. */
+uint64_t magot_plan_algorithmic_bytes(const magot_plan* p);
+
+/*
+ * Raw-sequence batch ops over n byte strings (seq_off has n+1 entries).
+ * Replaces: Sequence.reverse_compliment (genome.py:784-793).
+ * out must hold seq_off[n] bytes; record i lands at out[seq_off[i]...].
+ */
+int magot_revcomp_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
+                        uint8_t* out);
+
+/*
+ * Replaces: Sequence.translate (genome.py:795-822) for frame >= 0, strand
+ * '+'/'-'.  codons_out[i] = number of emitted residues (before trimX), or -1
+ * when the reference returns None (len <= 2 + frame).  pep_off (n+1) must be
+ * filled by magot_translate_sizes first; out holds pep_off[n] bytes.
+ * lut64 maps codon c0 + 4*c1 + 16*c2 (A=0,C=1,G=2,T=3) to a residue byte;
+ * NULL = the standard code of genome.py:795-802.  The junk first codon of
+ * frames 1/2 (genome.py:811-818) is emitted as 'X'.
+ */
+int magot_translate_sizes(const uint64_t* seq_off, uint64_t n, const int32_t* frames,
+                          uint64_t* pep_off, int64_t* codons_out);
+int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
+                          const int32_t* frames, const uint8_t* strands, const uint8_t* lut64,
+                          const uint64_t* pep_off, uint8_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAGOT_H */

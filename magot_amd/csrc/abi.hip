@@ -1,0 +1,569 @@
+// C ABI of libmagot.so (declarations and contracts: include/magot.h).
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <memory>
+
+#include "common.h"
+
+namespace magot {
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+void standard_lut(uint8_t out[64]) {
+  // genome.py:795-802, walked in TCAG order (first, second, third base).
+  static const char kAA[] = "FFLLSSSSYY**CC*WLLLLPPPPHHQQRRRRIIIMTTTTNNKKSSRRVVVVAAAADDEEGGGG";
+  static const int kTcagToCode[4] = {3, 1, 0, 2};  // T C A G -> A=0 C=1 G=2 T=3
+  int n = 0;
+  for (int a = 0; a < 4; ++a)
+    for (int b = 0; b < 4; ++b)
+      for (int c = 0; c < 4; ++c) {
+        int x = kTcagToCode[a] + 4 * kTcagToCode[b] + 16 * kTcagToCode[c];
+        out[x] = (uint8_t)kAA[n++];
+      }
+}
+
+}  // namespace magot
+
+using namespace magot;
+
+struct magot_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+struct magot_genome {
+  magot_ctx* ctx = nullptr;
+  void* arena = nullptr;
+  uint64_t arena_bytes = 0;
+  uint32_t* codes = nullptr;
+  uint32_t* lower = nullptr;
+  ExcRun* runs = nullptr;
+  uint32_t* dir = nullptr;
+  std::vector<uint64_t> contig_base, contig_len;
+  uint64_t extent = 0, total_bases = 0, n_runs = 0;
+};
+
+struct magot_plan {
+  magot_ctx* ctx = nullptr;
+  const magot_genome* g = nullptr;
+  void* arena = nullptr;
+  uint64_t arena_bytes = 0;
+  ExtractArgs args{};
+  std::vector<uint64_t> nuc_off, pep_off;  // host copies, n_tx+1
+  uint64_t n_exons = 0, n_tx = 0;
+  bool executed = false;
+};
+
+namespace {
+
+// Sub-allocate 256-byte aligned slices of one device allocation.
+struct Carve {
+  uint64_t used = 0;
+  template <class T>
+  uint64_t take(uint64_t count) {
+    uint64_t at = used;
+    used += (count * sizeof(T) + 255) & ~255ull;
+    return at;
+  }
+};
+
+int bind(magot_ctx* ctx) {
+  if (!ctx) {
+    set_error("null context");
+    return MAGOT_ERR_ARG;
+  }
+  MAGOT_HIP_TRY(hipSetDevice(ctx->device));
+  return MAGOT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int magot_abi_version(void) { return MAGOT_ABI_VERSION; }
+
+const char* magot_last_error(void) { return g_last_error.c_str(); }
+
+int magot_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int magot_ctx_create(int device, magot_ctx** out) {
+  if (!out) {
+    set_error("magot_ctx_create: null out");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  int n = 0;
+  MAGOT_HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) {
+    set_error("magot_ctx_create: device " + std::to_string(device) + " out of range (" +
+              std::to_string(n) + " visible)");
+    return MAGOT_ERR_ARG;
+  }
+  std::unique_ptr<magot_ctx> c(new magot_ctx());
+  c->device = device;
+  MAGOT_HIP_TRY(hipSetDevice(device));
+  MAGOT_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  MAGOT_HIP_TRY(hipEventCreate(&c->ev0));
+  MAGOT_HIP_TRY(hipEventCreate(&c->ev1));
+  *out = c.release();
+  return MAGOT_OK;
+}
+
+void magot_ctx_destroy(magot_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int magot_ctx_sync(magot_ctx* ctx) {
+  if (int rc = bind(ctx)) return rc;
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return MAGOT_OK;
+}
+
+int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
+                      uint32_t n_contigs, magot_genome** out) {
+  if (int rc = bind(ctx)) return rc;
+  if (!out || (n_contigs && (!seqs || !lens))) {
+    set_error("magot_genome_load: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  for (uint32_t i = 0; i < n_contigs; ++i)
+    if (lens[i] && !seqs[i]) {
+      set_error("magot_genome_load: null contig pointer");
+      return MAGOT_ERR_ARG;
+    }
+  HostPacked hp;
+  pack_genome(seqs, lens, n_contigs, &hp);
+  if (hp.runs.size() >= (size_t)kDirClean) {
+    set_error("magot_genome_load: too many exception runs");
+    return MAGOT_ERR_ARG;
+  }
+  std::unique_ptr<magot_genome> g(new magot_genome());
+  g->ctx = ctx;
+  Carve cv;
+  uint64_t o_codes = cv.take<uint32_t>(hp.codes.size());
+  uint64_t o_lower = cv.take<uint32_t>(hp.lower.size());
+  uint64_t o_runs = cv.take<ExcRun>(hp.runs.size());
+  uint64_t o_dir = cv.take<uint32_t>(hp.dir.size());
+  MAGOT_HIP_TRY(hipMalloc(&g->arena, cv.used));
+  g->arena_bytes = cv.used;
+  char* base = static_cast<char*>(g->arena);
+  g->codes = reinterpret_cast<uint32_t*>(base + o_codes);
+  g->lower = reinterpret_cast<uint32_t*>(base + o_lower);
+  g->runs = reinterpret_cast<ExcRun*>(base + o_runs);
+  g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
+  MAGOT_HIP_TRY(hipMemcpy(g->codes, hp.codes.data(), hp.codes.size() * 4, hipMemcpyHostToDevice));
+  MAGOT_HIP_TRY(hipMemcpy(g->lower, hp.lower.data(), hp.lower.size() * 4, hipMemcpyHostToDevice));
+  MAGOT_HIP_TRY(hipMemcpy(g->runs, hp.runs.data(), hp.runs.size() * sizeof(ExcRun),
+                          hipMemcpyHostToDevice));
+  MAGOT_HIP_TRY(hipMemcpy(g->dir, hp.dir.data(), hp.dir.size() * 4, hipMemcpyHostToDevice));
+  g->contig_base = std::move(hp.contig_base);
+  g->contig_len = std::move(hp.contig_len);
+  g->extent = hp.extent;
+  g->total_bases = hp.extent - kOrigin;
+  g->n_runs = hp.runs.size() - 1;
+  *out = g.release();
+  return MAGOT_OK;
+}
+
+int magot_genome_stats(const magot_genome* g, uint64_t* total_bases, uint64_t* n_exc_runs,
+                       uint64_t* device_bytes) {
+  if (!g) {
+    set_error("magot_genome_stats: null genome");
+    return MAGOT_ERR_ARG;
+  }
+  if (total_bases) *total_bases = g->total_bases;
+  if (n_exc_runs) *n_exc_runs = g->n_runs;
+  if (device_bytes) *device_bytes = g->arena_bytes;
+  return MAGOT_OK;
+}
+
+void magot_genome_destroy(magot_genome* g) {
+  if (!g) return;
+  if (g->ctx) (void)hipSetDevice(g->ctx->device);
+  if (g->arena) (void)hipFree(g->arena);
+  delete g;
+}
+
+int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* exons,
+                      uint64_t n_exons, const magot_tx* txs, uint64_t n_tx, uint32_t outputs,
+                      magot_plan** out, uint64_t* nuc_bytes, uint64_t* pep_bytes) {
+  if (int rc = bind(ctx)) return rc;
+  if (!g || !out || (n_exons && !exons) || (n_tx && !txs)) {
+    set_error("magot_plan_create: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (outputs & ~(MAGOT_OUT_NUC | MAGOT_OUT_PEP)) {
+    set_error("magot_plan_create: unknown output flags");
+    return MAGOT_ERR_ARG;
+  }
+  if (n_tx >= 0xFFFFFFFFull || n_exons >= 0xFFFFFFFFull) {
+    set_error("magot_plan_create: table too large for one plan (split it)");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  const uint64_t E = n_exons, T = n_tx;
+  // --- host tables --------------------------------------------------------
+  std::vector<uint64_t> ex_g(E), ex_out(E + 1), tx_nuc(T + 1), tx_pep(T + 1);
+  uint64_t expect = 0, acc = 0;
+  for (uint64_t t = 0; t < T; ++t) {
+    if (txs[t].exon_begin != expect) {
+      set_error("magot_plan_create: record " + std::to_string(t) +
+                " does not start where the previous one ended");
+      return MAGOT_ERR_ARG;
+    }
+    expect += txs[t].n_exons;
+    if (expect > E) {
+      set_error("magot_plan_create: records reference more exons than given");
+      return MAGOT_ERR_ARG;
+    }
+  }
+  if (expect != E) {
+    set_error("magot_plan_create: exons not covered by records");
+    return MAGOT_ERR_ARG;
+  }
+  const uint64_t n_contigs = g->contig_base.size();
+  for (uint64_t e = 0; e < E; ++e) {
+    const magot_exon& x = exons[e];
+    const uint64_t st = x.start_rc & ~kRcBit;
+    if (x.contig >= n_contigs || st + x.len > g->contig_len[x.contig] ||
+        st > g->contig_len[x.contig]) {
+      set_error("magot_plan_create: exon " + std::to_string(e) + " outside its contig");
+      return MAGOT_ERR_RANGE;
+    }
+    ex_g[e] = (g->contig_base[x.contig] + st) | (x.start_rc & kRcBit);
+    ex_out[e] = acc;
+    acc += x.len;
+  }
+  ex_out[E] = acc;
+  const uint64_t B = acc;
+  uint64_t P = 0;
+  for (uint64_t t = 0; t < T; ++t) {
+    tx_nuc[t] = ex_out[txs[t].exon_begin];
+    tx_pep[t] = P;
+    const uint64_t L = ex_out[txs[t].exon_begin + txs[t].n_exons] - tx_nuc[t];
+    P += L / 3;
+  }
+  tx_nuc[T] = B;
+  tx_pep[T] = P;
+
+  const uint64_t n_tiles64 = (B + kTile - 1) / kTile;
+  if (n_tiles64 >= 0x7FFFFFFFull) {
+    set_error("magot_plan_create: output too large for one launch");
+    return MAGOT_ERR_ARG;
+  }
+  const uint32_t n_tiles = (uint32_t)n_tiles64;
+  std::vector<uint32_t> tile_ex(2 * (uint64_t)n_tiles + 2), tile_t(n_tiles + 1);
+  std::vector<uint64_t> tile_q(n_tiles + 1);
+  uint64_t e1 = 0, e2 = 0, tt = 0;
+  for (uint32_t k = 0; k < n_tiles; ++k) {
+    const uint64_t T0 = (uint64_t)k * kTile;
+    while (e1 < E && ex_out[e1 + 1] <= T0) ++e1;           // exon containing T0
+    const uint64_t lim = T0 + kTile + kHalo;
+    if (e2 < e1) e2 = e1;
+    while (e2 < E && ex_out[e2] < lim) ++e2;              // first exon starting past the halo
+    tile_ex[2 * k] = (uint32_t)e1;
+    tile_ex[2 * k + 1] = (uint32_t)e2;
+    while (tt < T && tx_nuc[tt + 1] <= T0) ++tt;           // record containing T0
+    tile_t[k] = (uint32_t)tt;
+    const uint64_t into = T0 - tx_nuc[tt];
+    tile_q[k] = tx_pep[tt] + std::min((into + 2) / 3, tx_pep[tt + 1] - tx_pep[tt]);
+  }
+  tile_t[n_tiles] = T ? (uint32_t)(T - 1) : 0;
+  tile_q[n_tiles] = P;
+
+  // --- device arena ---------------------------------------------------------
+  std::unique_ptr<magot_plan> p(new magot_plan());
+  p->ctx = ctx;
+  p->g = g;
+  Carve cv;
+  const uint64_t o_exg = cv.take<uint64_t>(E + 1);
+  const uint64_t o_exo = cv.take<uint64_t>(E + 1);
+  const uint64_t o_txn = cv.take<uint64_t>(T + 1);
+  const uint64_t o_txp = cv.take<uint64_t>(T + 1);
+  const uint64_t o_tex = cv.take<uint32_t>(tile_ex.size());
+  const uint64_t o_tq = cv.take<uint64_t>(tile_q.size());
+  const uint64_t o_tt = cv.take<uint32_t>(tile_t.size());
+  const uint64_t o_nuc = cv.take<uint8_t>((outputs & MAGOT_OUT_NUC) ? B + 64 : 64);
+  const uint64_t o_pep = cv.take<uint8_t>((outputs & MAGOT_OUT_PEP) ? P + 64 : 64);
+  MAGOT_HIP_TRY(hipMalloc(&p->arena, cv.used));
+  p->arena_bytes = cv.used;
+  char* base = static_cast<char*>(p->arena);
+  auto up = [&](uint64_t off, const void* src, uint64_t bytes) -> hipError_t {
+    if (!bytes) return hipSuccess;
+    return hipMemcpy(base + off, src, bytes, hipMemcpyHostToDevice);
+  };
+  MAGOT_HIP_TRY(up(o_exg, ex_g.data(), E * 8));
+  MAGOT_HIP_TRY(up(o_exo, ex_out.data(), (E + 1) * 8));
+  MAGOT_HIP_TRY(up(o_txn, tx_nuc.data(), (T + 1) * 8));
+  MAGOT_HIP_TRY(up(o_txp, tx_pep.data(), (T + 1) * 8));
+  MAGOT_HIP_TRY(up(o_tex, tile_ex.data(), tile_ex.size() * 4));
+  MAGOT_HIP_TRY(up(o_tq, tile_q.data(), tile_q.size() * 8));
+  MAGOT_HIP_TRY(up(o_tt, tile_t.data(), tile_t.size() * 4));
+
+  ExtractArgs& a = p->args;
+  a.codes = g->codes;
+  a.lower = g->lower;
+  a.runs = g->runs;
+  a.dir = g->dir;
+  a.ex_g = reinterpret_cast<const uint64_t*>(base + o_exg);
+  a.ex_out = reinterpret_cast<const uint64_t*>(base + o_exo);
+  a.tx_nuc = reinterpret_cast<const uint64_t*>(base + o_txn);
+  a.tx_pep = reinterpret_cast<const uint64_t*>(base + o_txp);
+  a.tile_ex = reinterpret_cast<const uint32_t*>(base + o_tex);
+  a.tile_q = reinterpret_cast<const uint64_t*>(base + o_tq);
+  a.tile_t = reinterpret_cast<const uint32_t*>(base + o_tt);
+  a.nuc = reinterpret_cast<uint8_t*>(base + o_nuc);
+  a.pep = reinterpret_cast<uint8_t*>(base + o_pep);
+  a.total_nuc = B;
+  a.total_pep = P;
+  a.n_tiles = n_tiles;
+  a.outputs = outputs;
+  uint8_t lut[64];
+  standard_lut(lut);
+  std::memcpy(a.lut, lut, 64);
+
+  p->nuc_off = std::move(tx_nuc);
+  p->pep_off = std::move(tx_pep);
+  p->n_exons = E;
+  p->n_tx = T;
+  if (nuc_bytes) *nuc_bytes = B;
+  if (pep_bytes) *pep_bytes = P;
+  *out = p.release();
+  return MAGOT_OK;
+}
+
+void magot_plan_destroy(magot_plan* p) {
+  if (!p) return;
+  if (p->ctx) (void)hipSetDevice(p->ctx->device);
+  if (p->arena) (void)hipFree(p->arena);
+  delete p;
+}
+
+int magot_plan_execute(magot_ctx* ctx, magot_plan* p) {
+  if (int rc = bind(ctx)) return rc;
+  if (!p) {
+    set_error("magot_plan_execute: null plan");
+    return MAGOT_ERR_ARG;
+  }
+  launch_extract(p->args, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  p->executed = true;
+  return MAGOT_OK;
+}
+
+int magot_plan_fetch(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off,
+                     uint8_t* pep_out, uint64_t* pep_off) {
+  if (int rc = bind(ctx)) return rc;
+  if (!p) {
+    set_error("magot_plan_fetch: null plan");
+    return MAGOT_ERR_ARG;
+  }
+  if (!p->executed) {
+    set_error("magot_plan_fetch: plan not executed");
+    return MAGOT_ERR_STATE;
+  }
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (nuc_out && p->args.total_nuc) {
+    if (!(p->args.outputs & MAGOT_OUT_NUC)) {
+      set_error("magot_plan_fetch: plan built without MAGOT_OUT_NUC");
+      return MAGOT_ERR_STATE;
+    }
+    MAGOT_HIP_TRY(hipMemcpy(nuc_out, p->args.nuc, p->args.total_nuc, hipMemcpyDeviceToHost));
+  }
+  if (pep_out && p->args.total_pep) {
+    if (!(p->args.outputs & MAGOT_OUT_PEP)) {
+      set_error("magot_plan_fetch: plan built without MAGOT_OUT_PEP");
+      return MAGOT_ERR_STATE;
+    }
+    MAGOT_HIP_TRY(hipMemcpy(pep_out, p->args.pep, p->args.total_pep, hipMemcpyDeviceToHost));
+  }
+  if (nuc_off) std::memcpy(nuc_off, p->nuc_off.data(), p->nuc_off.size() * 8);
+  if (pep_off) std::memcpy(pep_off, p->pep_off.data(), p->pep_off.size() * 8);
+  return MAGOT_OK;
+}
+
+int magot_run(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off, uint8_t* pep_out,
+              uint64_t* pep_off) {
+  if (int rc = magot_plan_execute(ctx, p)) return rc;
+  return magot_plan_fetch(ctx, p, nuc_out, nuc_off, pep_out, pep_off);
+}
+
+int magot_plan_time(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms) {
+  if (int rc = bind(ctx)) return rc;
+  if (!p || iters <= 0 || !avg_ms) {
+    set_error("magot_plan_time: bad argument");
+    return MAGOT_ERR_ARG;
+  }
+  double total = 0.0;
+  for (int i = 0; i < iters; ++i) {
+    MAGOT_HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    launch_extract(p->args, ctx->stream);
+    MAGOT_HIP_TRY(hipGetLastError());
+    MAGOT_HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    MAGOT_HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0.f;
+    MAGOT_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    total += ms;
+  }
+  p->executed = true;
+  *avg_ms = total / iters;
+  return MAGOT_OK;
+}
+
+int magot_plan_device_outputs(magot_plan* p, void** nuc_dev, void** pep_dev) {
+  if (!p) {
+    set_error("magot_plan_device_outputs: null plan");
+    return MAGOT_ERR_ARG;
+  }
+  if (nuc_dev) *nuc_dev = p->args.nuc;
+  if (pep_dev) *pep_dev = p->args.pep;
+  return MAGOT_OK;
+}
+
+uint64_t magot_plan_algorithmic_bytes(const magot_plan* p) {
+  if (!p) return 0;
+  const uint64_t B = p->args.total_nuc, P = p->args.total_pep;
+  uint64_t bytes = (B + 3) / 4 + 16 * p->n_exons + 32 * p->n_tx;
+  if (p->args.outputs & MAGOT_OUT_NUC) bytes += B;
+  if (p->args.outputs & MAGOT_OUT_PEP) bytes += P;
+  return bytes;
+}
+
+int magot_revcomp_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
+                        uint8_t* out) {
+  if (int rc = bind(ctx)) return rc;
+  if (!seq_off || (n && (!seqs || !out))) {
+    set_error("magot_revcomp_batch: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  const uint64_t total = n ? seq_off[n] : 0;
+  if (total == 0) return MAGOT_OK;
+  for (uint64_t i = 0; i < n; ++i)
+    if (seq_off[i + 1] < seq_off[i]) {
+      set_error("magot_revcomp_batch: offsets not monotone");
+      return MAGOT_ERR_ARG;
+    }
+  void* d = nullptr;
+  const uint64_t off_bytes = (n + 1) * 8, pad = 64;
+  MAGOT_HIP_TRY(hipMalloc(&d, 2 * (total + pad) + off_bytes));
+  uint8_t* d_in = static_cast<uint8_t*>(d);
+  uint8_t* d_out = d_in + total + pad;
+  uint64_t* d_off = reinterpret_cast<uint64_t*>(d_out + total + pad);
+  int rc = MAGOT_OK;
+  hipError_t e = hipMemcpyAsync(d_in, seqs, total, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(d_off, seq_off, off_bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) {
+    launch_revcomp(d_in, d_off, n, total, d_out, ctx->stream);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, total, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    set_error(std::string("magot_revcomp_batch: ") + hipGetErrorString(e));
+    rc = MAGOT_ERR_HIP;
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
+int magot_translate_sizes(const uint64_t* seq_off, uint64_t n, const int32_t* frames,
+                          uint64_t* pep_off, int64_t* codons_out) {
+  if (!seq_off || !pep_off || (n && !frames)) {
+    set_error("magot_translate_sizes: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  uint64_t acc = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const int64_t f = frames[i];
+    if (f < 0) {
+      set_error("magot_translate_sizes: negative frame");
+      return MAGOT_ERR_ARG;
+    }
+    const int64_t L = (int64_t)(seq_off[i + 1] - seq_off[i]);
+    int64_t c = -1;
+    if (L > 2 + f) {
+      const int64_t pe = f + ((2 - 2 * f) % 3 + 3) % 3;
+      c = 1 + (L - 1 - pe) / 3;
+    }
+    pep_off[i] = acc;
+    if (codons_out) codons_out[i] = c;
+    if (c > 0) acc += (uint64_t)c;
+  }
+  pep_off[n] = acc;
+  return MAGOT_OK;
+}
+
+int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
+                          const int32_t* frames, const uint8_t* strands, const uint8_t* lut64,
+                          const uint64_t* pep_off, uint8_t* out) {
+  if (int rc = bind(ctx)) return rc;
+  if (!seq_off || !pep_off || (n && (!frames || !strands))) {
+    set_error("magot_translate_batch: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (strands[i] != '+' && strands[i] != '-') {
+      set_error("magot_translate_batch: strand must be '+' or '-'");
+      return MAGOT_ERR_ARG;
+    }
+  const uint64_t total = n ? seq_off[n] : 0, total_pep = n ? pep_off[n] : 0;
+  if (total_pep == 0) return MAGOT_OK;
+  if (!seqs || !out) {
+    set_error("magot_translate_batch: null buffer");
+    return MAGOT_ERR_ARG;
+  }
+  uint8_t lut[64];
+  if (lut64) std::memcpy(lut, lut64, 64);
+  else standard_lut(lut);
+  uint32_t lut16[16];
+  std::memcpy(lut16, lut, 64);
+  const uint64_t pad = 64, ob = (n + 1) * 8;
+  const uint64_t bytes = (total + pad) + (total_pep + pad) + 2 * ob + n * 4 + n + pad;
+  void* d = nullptr;
+  MAGOT_HIP_TRY(hipMalloc(&d, bytes));
+  uint8_t* d_in = static_cast<uint8_t*>(d);
+  uint8_t* d_out = d_in + total + pad;
+  uint64_t* d_off = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(d_out + total_pep + pad) + 7) & ~7ull);
+  uint64_t* d_poff = d_off + (n + 1);
+  int32_t* d_fr = reinterpret_cast<int32_t*>(d_poff + (n + 1));
+  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_fr + n);
+  hipError_t e = hipSuccess;
+  if (total) e = hipMemcpyAsync(d_in, seqs, total, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_off, seq_off, ob, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_poff, pep_off, ob, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_fr, frames, n * 4, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_st, strands, n, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) {
+    launch_translate(d_in, d_off, n, d_fr, d_st, d_poff, total_pep, lut16, d_out, ctx->stream);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, total_pep, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  int rc = MAGOT_OK;
+  if (e != hipSuccess) {
+    set_error(std::string("magot_translate_batch: ") + hipGetErrorString(e));
+    rc = MAGOT_ERR_HIP;
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
+}  // extern "C"

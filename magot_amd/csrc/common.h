@@ -1,0 +1,108 @@
+// Internal definitions shared by the libmagot translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/magot.h"
+
+namespace magot {
+
+// ---------------------------------------------------------------------------
+// Genome layout in HBM
+// ---------------------------------------------------------------------------
+// All contigs live in one global base coordinate space.  Coordinate 0 is
+// preceded by kOrigin pad bases so that a 16-base window ending at any real
+// base never starts below 0 (the reverse-strand gather reads [hi-15, hi]).
+constexpr uint64_t kOrigin = 64;
+// Exception-run directory granularity: one u32 per 4096 bases.
+constexpr int kDirShift = 12;
+constexpr uint32_t kDirClean = 0x80000000u;  // no run touches this block
+constexpr uint64_t kRcBit = 1ull << 63;
+
+// A maximal run of one byte that is not in ACGTacgt (N, n, IUPAC, '-', ' ' ...).
+struct ExcRun {
+  uint64_t start;  // global coordinate of the first base
+  uint32_t len;
+  uint32_t byte;   // the raw byte
+};
+static_assert(sizeof(ExcRun) == 16, "ExcRun must be 16 bytes");
+
+struct HostPacked {
+  std::vector<uint32_t> codes;    // 16 bases per word, base i at bits 2*(i&15)
+  std::vector<uint32_t> lower;    // 32 bases per word, 1 = soft-masked (lowercase)
+  std::vector<ExcRun> runs;       // sorted by start, sentinel appended
+  std::vector<uint32_t> dir;      // per 4096-block first run with end > block start
+  std::vector<uint64_t> contig_base;
+  std::vector<uint64_t> contig_len;
+  uint64_t extent = 0;            // first coordinate past the last contig
+};
+
+// Packs raw contig bytes (multi-threaded host code, pack.cpp).
+void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, HostPacked* out);
+
+// ---------------------------------------------------------------------------
+// Extraction tiling
+// ---------------------------------------------------------------------------
+constexpr int kThreads = 256;                 // one workgroup = 4 waves
+constexpr int kChunk = 16;                    // bytes per lane-store
+constexpr int kChunksPerThread = 3;
+constexpr int kTile = kThreads * kChunk * kChunksPerThread;   // 12288 nucleotide bytes
+constexpr int kHalo = kChunk;                 // codons may run 2 bytes past the tile
+constexpr int kTileChunks = kTile / kChunk;   // 768
+constexpr int kExonCap = 512;                 // exons cached in LDS per tile
+
+struct ExtractArgs {
+  const uint32_t* codes;
+  const uint32_t* lower;
+  const ExcRun* runs;
+  const uint32_t* dir;
+  const uint64_t* ex_g;       // per exon: global start | kRcBit
+  const uint64_t* ex_out;     // n_exons+1 output prefix offsets
+  const uint64_t* tx_nuc;     // n_tx+1
+  const uint64_t* tx_pep;     // n_tx+1
+  const uint32_t* tile_ex;    // 2 per tile: [first exon, end exon)
+  const uint64_t* tile_q;     // n_tiles+1: first residue produced by the tile
+  const uint32_t* tile_t;     // n_tiles+1: record containing the tile start
+  uint8_t* nuc;
+  uint8_t* pep;
+  uint64_t total_nuc;
+  uint64_t total_pep;
+  uint32_t n_tiles;
+  uint32_t outputs;
+  uint32_t lut[16];           // 64 residue bytes indexed c0 + 4*c1 + 16*c2
+};
+
+void launch_extract(const ExtractArgs& a, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Raw sequence batch ops (seqops.hip)
+// ---------------------------------------------------------------------------
+void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t total,
+                    uint8_t* out, hipStream_t s);
+void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const int32_t* frames,
+                      const uint8_t* strands, const uint64_t* pep_off, uint64_t total_pep,
+                      const uint32_t* lut16, uint8_t* out, hipStream_t s);
+
+// Standard genetic code (genome.py:795-802) as a 64-byte table indexed
+// c0 + 4*c1 + 16*c2 with A=0, C=1, G=2, T=3.
+void standard_lut(uint8_t out[64]);
+
+// ---------------------------------------------------------------------------
+// Errors
+// ---------------------------------------------------------------------------
+void set_error(const std::string& msg);
+
+}  // namespace magot
+
+#define MAGOT_HIP_TRY(expr)                                                      \
+  do {                                                                           \
+    hipError_t e_ = (expr);                                                      \
+    if (e_ != hipSuccess) {                                                      \
+      ::magot::set_error(std::string(#expr) + ": " + hipGetErrorString(e_));     \
+      return MAGOT_ERR_HIP;                                                      \
+    }                                                                            \
+  } while (0)

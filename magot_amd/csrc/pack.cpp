@@ -1,0 +1,152 @@
+// Host-side genome packer: raw contig bytes -> 2-bit code plane, soft-mask
+// plane, exception runs and their block directory (layout: common.h).
+//
+// The bytes packed are exactly what GenomeSequence keeps (genome.py:870-877):
+// every byte of every sequence line except CR/LF, case preserved.  ACGTacgt
+// become codes; every other byte value is kept verbatim in a run list, so the
+// device path can reproduce any input byte exactly.
+#include <algorithm>
+#include <atomic>
+#include <thread>
+
+#include "common.h"
+
+namespace magot {
+namespace {
+
+struct ByteClass {
+  uint8_t code[256];
+  uint8_t lower[256];
+  uint8_t plain[256];  // 1 for ACGTacgt
+  ByteClass() {
+    for (int i = 0; i < 256; ++i) {
+      code[i] = 0;
+      lower[i] = 0;
+      plain[i] = 0;
+    }
+    const char up[4] = {'A', 'C', 'G', 'T'};
+    for (int c = 0; c < 4; ++c) {
+      code[(uint8_t)up[c]] = (uint8_t)c;
+      plain[(uint8_t)up[c]] = 1;
+      code[(uint8_t)(up[c] | 0x20)] = (uint8_t)c;
+      plain[(uint8_t)(up[c] | 0x20)] = 1;
+      lower[(uint8_t)(up[c] | 0x20)] = 1;
+    }
+  }
+};
+
+const ByteClass& byte_class() {
+  static const ByteClass k;
+  return k;
+}
+
+// Pack global coordinates [p0, p1) (p0, p1 multiples of 32, so no code or
+// mask word is shared with another piece).
+void pack_piece(const uint8_t* const* seqs, const HostPacked& layout, uint64_t p0, uint64_t p1,
+                uint32_t* codes, uint32_t* lower, std::vector<ExcRun>* runs) {
+  const ByteClass& bc = byte_class();
+  const auto& base = layout.contig_base;
+  const auto& len = layout.contig_len;
+  size_t n = base.size();
+  // first contig whose end > p0
+  size_t c = std::upper_bound(base.begin(), base.end(), p0) - base.begin();
+  c = c == 0 ? 0 : c - 1;
+  ExcRun cur{0, 0, 0};
+  bool open = false;
+  for (; c < n; ++c) {
+    uint64_t cb = base[c], ce = base[c] + len[c];
+    if (cb >= p1) break;
+    uint64_t lo = std::max(cb, p0), hi = std::min(ce, p1);
+    if (lo >= hi) continue;
+    const uint8_t* s = seqs[c] + (lo - cb);
+    for (uint64_t g = lo; g < hi; ++g) {
+      uint8_t b = *s++;
+      if (bc.plain[b]) {
+        codes[g >> 4] |= (uint32_t)bc.code[b] << (2 * (g & 15));
+        lower[g >> 5] |= (uint32_t)bc.lower[b] << (g & 31);
+        if (open) {
+          runs->push_back(cur);
+          open = false;
+        }
+      } else {
+        if (open && cur.byte == b && cur.start + cur.len == g && cur.len < 0x7fffffffu) {
+          ++cur.len;
+        } else {
+          if (open) runs->push_back(cur);
+          cur = ExcRun{g, 1, b};
+          open = true;
+        }
+      }
+    }
+  }
+  if (open) runs->push_back(cur);
+}
+
+}  // namespace
+
+void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, HostPacked* out) {
+  out->contig_base.resize(n);
+  out->contig_len.resize(n);
+  uint64_t cur = kOrigin;
+  for (uint32_t i = 0; i < n; ++i) {
+    out->contig_base[i] = cur;
+    out->contig_len[i] = lens[i];
+    cur += lens[i];
+  }
+  out->extent = cur;
+  const uint64_t padded = cur + 64;
+  out->codes.assign(padded / 16 + 4, 0u);
+  out->lower.assign(padded / 32 + 4, 0u);
+
+  // Split [0, extent) into 32-aligned pieces for the worker threads.
+  unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
+  const uint64_t min_piece = 1ull << 22;
+  uint64_t npieces = std::max<uint64_t>(1, std::min<uint64_t>(hw * 4, cur / min_piece + 1));
+  uint64_t step = ((cur + npieces - 1) / npieces + 31) & ~31ull;
+  std::vector<std::vector<ExcRun>> piece_runs(npieces);
+  std::vector<std::thread> pool;
+  std::atomic<uint64_t> next{0};
+  auto worker = [&]() {
+    for (;;) {
+      uint64_t k = next.fetch_add(1);
+      if (k >= npieces) return;
+      uint64_t p0 = k * step, p1 = std::min(cur, p0 + step);
+      if (p0 < p1)
+        pack_piece(seqs, *out, p0, p1, out->codes.data(), out->lower.data(), &piece_runs[k]);
+    }
+  };
+  unsigned nthreads = (unsigned)std::min<uint64_t>(hw, npieces);
+  for (unsigned t = 0; t < nthreads; ++t) pool.emplace_back(worker);
+  for (auto& t : pool) t.join();
+
+  // Concatenate, merging runs split at piece boundaries.
+  out->runs.clear();
+  for (auto& pr : piece_runs) {
+    for (const ExcRun& r : pr) {
+      if (!out->runs.empty()) {
+        ExcRun& last = out->runs.back();
+        if (last.byte == r.byte && last.start + last.len == r.start &&
+            (uint64_t)last.len + r.len < 0x7fffffffull) {
+          last.len += r.len;
+          continue;
+        }
+      }
+      out->runs.push_back(r);
+    }
+  }
+  out->runs.push_back(ExcRun{~0ull, 0, 0});  // sentinel
+
+  // Directory: first run whose end lies past the block start.
+  const uint64_t nblocks = ((padded + 4095) >> kDirShift) + 2;
+  out->dir.assign(nblocks, 0);
+  size_t r = 0, nr = out->runs.size() - 1;
+  for (uint64_t b = 0; b < nblocks; ++b) {
+    uint64_t bs = b << kDirShift, be = bs + (1ull << kDirShift);
+    while (r < nr && out->runs[r].start + out->runs[r].len <= bs) ++r;
+    uint32_t v = (uint32_t)r;
+    if (out->runs[r].start >= be) v |= kDirClean;
+    out->dir[b] = v;
+  }
+}
+
+}  // namespace magot

@@ -1,0 +1,190 @@
+"""Device-level objects over the C ABI: packed genome, extraction plan, and the
+raw-sequence batch ops.  Everything here runs on the GPU through libmagot.so;
+there is no host compute path."""
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import EXON_DTYPE, TX_DTYPE, OUT_NUC, OUT_PEP, MagotError, check, ptr
+
+
+def _as_bytes(s):
+    if isinstance(s, (bytes, bytearray, memoryview)):
+        return bytes(s)
+    return s.encode('latin-1')
+
+
+class DeviceGenome(object):
+    """A GenomeSequence packed into HBM (magot_genome_load).
+
+    ``contigs`` is a list of (name, sequence) pairs; sequences are ``str``
+    (latin-1, one char per byte) or ``bytes``.
+    """
+
+    def __init__(self, contigs, ctx=None):
+        self.ctx = ctx or _lib.default_context()
+        names = []
+        bufs = []
+        for name, seq in contigs:
+            names.append(name)
+            bufs.append(np.frombuffer(_as_bytes(seq), dtype=np.uint8))
+        n = len(bufs)
+        self.names = names
+        self.index = {nm: i for i, nm in enumerate(names)}
+        self.lengths = np.array([len(b) for b in bufs], dtype=np.uint64)
+        ptrs = (ctypes.POINTER(ctypes.c_uint8) * max(n, 1))()
+        for i, b in enumerate(bufs):
+            if len(b):
+                ptrs[i] = b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))
+        lens = np.ascontiguousarray(self.lengths)
+        h = ctypes.c_void_p()
+        L = _lib.lib()
+        check(L.magot_genome_load(self.ctx.handle, ptrs, lens.ctypes.data_as(_lib._u64p), n,
+                                  ctypes.byref(h)), 'magot_genome_load')
+        self.handle = h
+        tb, nr, db = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        check(L.magot_genome_stats(h, ctypes.byref(tb), ctypes.byref(nr), ctypes.byref(db)),
+              'magot_genome_stats')
+        self.total_bases = tb.value
+        self.n_exception_runs = nr.value
+        self.device_bytes = db.value
+
+    def close(self):
+        if getattr(self, 'handle', None):
+            _lib.lib().magot_genome_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ExtractionPlan(object):
+    """Interval table -> device plan (magot_plan_create).
+
+    ``exons``: structured array of EXON_DTYPE in output order; ``txs``:
+    structured array of TX_DTYPE tiling it.  ``outputs``: OUT_NUC | OUT_PEP.
+    """
+
+    def __init__(self, genome, exons, txs, outputs=OUT_NUC | OUT_PEP):
+        self.genome = genome
+        self.ctx = genome.ctx
+        exons = np.ascontiguousarray(exons, dtype=EXON_DTYPE)
+        txs = np.ascontiguousarray(txs, dtype=TX_DTYPE)
+        self.n_exons = len(exons)
+        self.n_tx = len(txs)
+        self.outputs = outputs
+        h = ctypes.c_void_p()
+        nb, pb = ctypes.c_uint64(), ctypes.c_uint64()
+        check(_lib.lib().magot_plan_create(self.ctx.handle, genome.handle, ptr(exons),
+                                           self.n_exons, ptr(txs), self.n_tx, outputs,
+                                           ctypes.byref(h), ctypes.byref(nb), ctypes.byref(pb)),
+              'magot_plan_create')
+        self.handle = h
+        self.nuc_bytes = nb.value
+        self.pep_bytes = pb.value
+
+    def execute(self):
+        check(_lib.lib().magot_plan_execute(self.ctx.handle, self.handle), 'magot_plan_execute')
+
+    def sync(self):
+        self.ctx.sync()
+
+    def fetch(self):
+        """Returns (nuc uint8[B] or None, nuc_off uint64[T+1], pep uint8[P] or None,
+        pep_off uint64[T+1])."""
+        nuc = np.empty(self.nuc_bytes, dtype=np.uint8) if self.outputs & OUT_NUC else None
+        pep = np.empty(self.pep_bytes, dtype=np.uint8) if self.outputs & OUT_PEP else None
+        noff = np.empty(self.n_tx + 1, dtype=np.uint64)
+        poff = np.empty(self.n_tx + 1, dtype=np.uint64)
+        check(_lib.lib().magot_plan_fetch(self.ctx.handle, self.handle,
+                                          ptr(nuc) if nuc is not None and len(nuc) else None,
+                                          ptr(noff),
+                                          ptr(pep) if pep is not None and len(pep) else None,
+                                          ptr(poff)), 'magot_plan_fetch')
+        return nuc, noff, pep, poff
+
+    def run(self):
+        self.execute()
+        return self.fetch()
+
+    def time(self, iters):
+        ms = ctypes.c_double()
+        check(_lib.lib().magot_plan_time(self.ctx.handle, self.handle, int(iters),
+                                         ctypes.byref(ms)), 'magot_plan_time')
+        return ms.value
+
+    @property
+    def algorithmic_bytes(self):
+        return int(_lib.lib().magot_plan_algorithmic_bytes(self.handle))
+
+    def close(self):
+        if getattr(self, 'handle', None):
+            _lib.lib().magot_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _concat(seqs):
+    parts = [_as_bytes(s) for s in seqs]
+    off = np.zeros(len(parts) + 1, dtype=np.uint64)
+    if parts:
+        np.cumsum([len(p) for p in parts], out=off[1:])
+    buf = np.frombuffer(b''.join(parts), dtype=np.uint8) if parts else np.zeros(0, np.uint8)
+    return buf, off
+
+
+def revcomp_batch(seqs, ctx=None):
+    """Sequence.reverse_compliment (genome.py:784-793) over a list of strings."""
+    ctx = ctx or _lib.default_context()
+    buf, off = _concat(seqs)
+    out = np.empty(max(len(buf), 1), dtype=np.uint8)
+    check(_lib.lib().magot_revcomp_batch(ctx.handle, ptr(buf) if len(buf) else None, ptr(off),
+                                         len(seqs), ptr(out)), 'magot_revcomp_batch')
+    raw = out.tobytes()
+    return [raw[int(off[i]):int(off[i + 1])].decode('latin-1') for i in range(len(seqs))]
+
+
+def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
+    """Untrimmed Sequence.translate (genome.py:795-822) residues per input, or None
+    where the reference returns None.  The caller applies trimX."""
+    ctx = ctx or _lib.default_context()
+    n = len(seqs)
+    buf, off = _concat(seqs)
+    fr = np.ascontiguousarray(frames, dtype=np.int32)
+    st = np.frombuffer(''.join(strands).encode('latin-1'), dtype=np.uint8).copy() if n else \
+        np.zeros(0, np.uint8)
+    poff = np.empty(n + 1, dtype=np.uint64)
+    codons = np.empty(max(n, 1), dtype=np.int64)
+    L = _lib.lib()
+    check(L.magot_translate_sizes(ptr(off), n, ptr(fr), ptr(poff), ptr(codons)),
+          'magot_translate_sizes')
+    total = int(poff[n])
+    out = np.empty(max(total, 1), dtype=np.uint8)
+    lut = None
+    if lut64 is not None:
+        lut = np.frombuffer(bytes(lut64), dtype=np.uint8).copy()
+    check(L.magot_translate_batch(ctx.handle, ptr(buf) if len(buf) else None, ptr(off), n,
+                                  ptr(fr), ptr(st), ptr(lut), ptr(poff), ptr(out)),
+          'magot_translate_batch')
+    raw = out.tobytes()
+    res = []
+    for i in range(n):
+        if codons[i] < 0:
+            res.append(None)
+        else:
+            res.append(raw[int(poff[i]):int(poff[i + 1])].decode('latin-1'))
+    return res
+
+
+__all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'OUT_NUC',
+           'OUT_PEP', 'MagotError']

@@ -1,0 +1,129 @@
+"""Command-line tools on the extraction path (genome_tools.py of the reference).
+
+    python -m magot_amd.genome_tools gff2fasta <fasta> <gff> [seq_type=protein]
+           [longest=True] [genomic=True] [from_exons=True] [order=py2|insertion]
+    python -m magot_amd.genome_tools cds2pep <cds.fasta>
+
+Arguments follow the reference's CLI convention (genome_tools.py:25-45):
+positional values, then ``key=value`` pairs, all strings.  The reference
+``eval``s the assembled call; here values are parsed as Python literals
+(``True``/``False``/numbers) and never executed.
+
+Record order defaults to ``py2`` so the bytes written match the reference's
+own goldens (test_data/test_suite.py:12-13); ``order=insertion`` gives the
+Python-3 order.
+"""
+
+import ast
+import sys
+
+from . import engine
+from . import genome
+
+
+def _literal(text):
+    try:
+        return ast.literal_eval(text)
+    except (ValueError, SyntaxError):
+        return text
+
+
+def _write(text):
+    out = getattr(sys.stdout, 'buffer', None)
+    if out is not None:
+        sys.stdout.flush()
+        out.write(text.encode('latin-1'))
+        out.flush()
+    else:
+        sys.stdout.write(text)
+
+
+def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', longest='False',
+              genomic='False', order='py2'):
+    """genome_tools.py:324-330."""
+    g = genome.Genome(genome_sequence)
+    if from_exons == 'True':
+        # reference quirk kept: a str features_to_ignore is a substring test
+        g.read_gff(gff, features_to_ignore='CDS', features_to_replace=[('exon', 'CDS')])
+    else:
+        g.read_gff(gff)
+    text = g.annotations.get_fasta('gene', seq_type=seq_type, longest=_literal(longest),
+                                   genomic=_literal(genomic), order=order)
+    _write(text + '\n')
+
+
+def cds2pep(fasta_file):
+    """genome_tools.py:664-675: headers echoed, each record translated; all
+    records go to the GPU as one batch."""
+    events = []       # ('line', text) | ('pep', job index)
+    seqs = []
+    failure = None
+    work = []
+    for raw in genome.ensure_file(fasta_file):
+        line = raw.replace('\n', '').replace('\r', '')
+        try:
+            first = line[0]
+        except IndexError as e:
+            failure = e
+            break
+        if first == '>':
+            cur = ''.join(work)
+            if cur != '':
+                events.append(('pep', len(seqs)))
+                seqs.append(cur)
+                work = []
+            events.append(('line', line))
+        else:
+            work.append(line)
+    if failure is None:
+        events.append(('pep', len(seqs)))
+        seqs.append(''.join(work))
+    peps = engine.translate_batch(seqs, [0] * len(seqs), ['+'] * len(seqs)) if seqs else []
+    out = []
+    for kind, val in events:
+        if kind == 'line':
+            out.append(val)
+        else:
+            p = peps[val]
+            if p is not None and p[:1] == 'X':
+                p = p[1:]
+            out.append(str(p))
+    _write(''.join(s + '\n' for s in out))
+    if failure is not None:
+        raise failure
+
+
+TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep}
+
+
+def parse_argv(argv):
+    """['tool', 'pos', 'k=v', ...] -> (tool, positional, keywords) as the
+    reference's main() assembles them (genome_tools.py:35-44: only the text
+    between the first and second '=' is the value)."""
+    name = argv[0]
+    args, kw = [], {}
+    for a in argv[1:]:
+        if '=' in a:
+            parts = a.split('=')
+            kw[parts[0]] = parts[1]
+        else:
+            args.append(a)
+    return name, args, kw
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    if not argv or argv[0] in ('-h', '-help', '--help', 'help'):
+        sys.stdout.write(__doc__)
+        return 0
+    name, args, kw = parse_argv(argv)
+    if name not in TOOLS:
+        sys.stderr.write('unknown tool %r (extraction path tools: %s)\n'
+                         % (name, ', '.join(sorted(TOOLS))))
+        return 2
+    TOOLS[name](*args, **kw)
+    return 0
+
+
+if __name__ == '__main__':
+    sys.exit(main())

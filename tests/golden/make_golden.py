@@ -1,0 +1,254 @@
+"""Regenerate the golden vectors in tests/golden/*.json from the REFERENCE.
+
+Runs only in the build container (never on the GPU box): it needs the
+reference at /root/reference.  The reference is Python 2.7; importing it under
+Python 3.10 fails with an ordinary SyntaxError, so this script makes a
+mechanical lib2to3 copy in /tmp/magot_py3 (outside the repository) and imports
+that.  On this path the only Python-2/3 difference is dict iteration order,
+handled by re-ordering the gene dict with the Python-2 order model
+(oracle.magot_oracle.py2_order_after_deepcopy), which is itself pinned by
+test_data/test_suite.py:12-13 (see tests/test_oracle.py).
+
+Outputs (data only: inputs, expected outputs, hashes):
+  kat.json        Sequence.reverse_compliment / translate / get_orfs vectors
+  edge_cases.json get_fasta edge cases incl. stdout/exception
+  fixtures.json   hashes of whole-file gff2fasta outputs on the shipped data
+  synth_small.json hashes of gff2fasta on the seeded small synthetic
+
+Usage:  python tests/golden/make_golden.py
+"""
+
+import contextlib
+import hashlib
+import io
+import json
+import os
+import random
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import goldlib  # noqa: E402
+from oracle import magot_oracle as mo  # noqa: E402
+
+REF = '/root/reference'
+PY3 = '/tmp/magot_py3'
+REF_FILES = ['genome.py', 'genome_tools.py', 'genome_tools_config.py', 'magot_smallfuncs.py',
+             'magot_variants.py', 'annotation_funcs.py']
+
+
+def reference_module():
+    if not os.path.exists(os.path.join(PY3, 'genome.py')):
+        os.makedirs(PY3, exist_ok=True)
+        for f in REF_FILES:
+            shutil.copy(os.path.join(REF, f), PY3)
+            os.chmod(os.path.join(PY3, f), 0o644)
+        subprocess.check_call([sys.executable, '-m', 'lib2to3', '-w', '-n'] +
+                              [os.path.join(PY3, f) for f in REF_FILES],
+                              stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    sys.path.insert(0, PY3)
+    import genome as refgenome
+    return refgenome
+
+
+def sha(s):
+    if isinstance(s, str):
+        s = s.encode('latin-1')
+    return hashlib.sha256(s).hexdigest()
+
+
+def call(fn):
+    """(result, exception name, captured stdout)."""
+    buf = io.StringIO()
+    res = None
+    exc = None
+    with contextlib.redirect_stdout(buf):
+        try:
+            res = fn()
+        except Exception as e:  # noqa: BLE001
+            exc = type(e).__name__
+    return res, exc, buf.getvalue()
+
+
+# ---------------------------------------------------------------------------
+
+KAT_STRINGS = ['ATGGCCTTTAAACCCGGGTAG', 'NNNATGNNN', 'ATGRYKatgu', 'AT', 'ATGC',
+               'ACGTRYacgtn-*.', 'ATGAAAMTAGCCCATGGGTAA', 'ATGAAAATGTAGCCCATGGGTAA', '', 'A',
+               'ATG', 'atgaaatag', 'XATGCCC', 'ATGCCCGGGTTTAAACCC' * 3]
+
+
+def make_kat(ref):
+    rnd = random.Random(1015)
+    alpha = 'ACGTACGTACGTacgtNnRYKMSW-.* U'
+    strs = list(KAT_STRINGS)
+    for n in list(range(0, 12)) + [17, 30, 31, 32, 33, 47, 48, 49, 64, 100]:
+        for _ in range(3):
+            strs.append(''.join(rnd.choice(alpha) for _ in range(n)))
+    out = []
+    for s in strs:
+        S = ref.Sequence(s)
+        rec = {'seq': s, 'revcomp': S.reverse_compliment(), 'translate': {}, 'orfs': {}}
+        for frame in range(5):
+            for strand in '+-':
+                for trim in (True, False):
+                    r, e, _ = call(lambda: S.translate(frame=frame, strand=strand, trimX=trim))
+                    rec['translate']['%d%s%d' % (frame, strand, int(trim))] = \
+                        {'exc': e} if e else r
+        for longest in (False, True):
+            for atg in (False, True):
+                r, e, _ = call(lambda: S.get_orfs(longest=longest, from_atg=atg))
+                rec['orfs']['%d%d' % (int(longest), int(atg))] = {'exc': e} if e else r
+        out.append(rec)
+    return out
+
+
+# ---------------------------------------------------------------------------
+
+EDGE_GENOME = '>c1\nACGTACGTAAccggttNNRYacgtACGTAAATTTGGGCCC\n>c2 desc\nGGGAAATTTCCCgggaaatttccc\n'
+
+
+def _gtf_line(seqid, start, end, strand, tid, gid, ftype='CDS'):
+    return '%s\tt\t%s\t%d\t%d\t.\t%s\t0\ttranscript_id "%s"; gene_id "%s";\n' % (
+        seqid, ftype, start, end, strand, tid, gid)
+
+
+def _gff3(seqid, ftype, start, end, strand, attrs):
+    return '%s\tt\t%s\t%d\t%d\t.\t%s\t.\t%s\n' % (seqid, ftype, start, end, strand, attrs)
+
+
+def edge_case_inputs():
+    g3h = _gff3('c1', 'gene', 1, 40, '+', 'ID=g') + _gff3('c1', 'mRNA', 1, 40, '+', 'ID=t;Parent=g')
+
+    def cds(*ivs):
+        return ''.join(_gff3(sid, 'CDS', a, b, s, 'ID=c;Parent=t') for sid, a, b, s in ivs)
+
+    cases = {
+        'dup_coords': g3h + cds(('c1', 1, 6, '+'), ('c1', 1, 6, '+'), ('c1', 10, 20, '+')),
+        'minus_iupac': g3h + cds(('c1', 1, 6, '-'), ('c1', 10, 20, '-')),
+        'mixed_strand': g3h + cds(('c1', 1, 6, '-'), ('c1', 10, 20, '+')),
+        'mixed_strand_rev': g3h + cds(('c1', 1, 6, '+'), ('c1', 10, 20, '-')),
+        'dot_strand': g3h + cds(('c1', 1, 6, '.')),
+        'past_end': g3h + cds(('c1', 35, 99, '+')),
+        'past_end_minus': g3h + cds(('c1', 35, 99, '-')),
+        'start_zero': g3h + cds(('c1', 0, 5, '+')),
+        'start_zero_past_end': g3h + cds(('c1', 0, 50, '+')),
+        'reversed_coords': g3h + cds(('c1', 6, 1, '+')),
+        'protein_n_codons': g3h + cds(('c1', 15, 20, '+'), ('c1', 1, 9, '+')),
+        'protein_short': g3h + cds(('c1', 1, 2, '+')),
+        'protein_len3_minus': g3h + cds(('c1', 18, 20, '-')),
+        'bad_strand': g3h + cds(('c1', 1, 6, '?')),
+        'missing_seqid': g3h + cds(('cX', 1, 6, '+')),
+        'desc_seqid': _gff3('c2 desc', 'gene', 1, 9, '+', 'ID=g') +
+        _gff3('c2 desc', 'mRNA', 1, 9, '+', 'ID=t;Parent=g') +
+        _gff3('c2 desc', 'CDS', 1, 9, '+', 'ID=c;Parent=t'),
+        'nine_tabs': g3h + cds(('c1', 1, 6, '+')).replace('\n', '\textra\n'),
+        'gene_no_cds': g3h + _gff3('c1', 'gene', 1, 5, '+', 'ID=g2') + cds(('c1', 1, 6, '+')),
+        'utr_after_cds': g3h + cds(('c1', 1, 6, '+')) +
+        _gff3('c1', 'UTR', 7, 9, '+', 'ID=u;Parent=t'),
+        'utr_first': g3h + _gff3('c1', 'UTR', 7, 9, '+', 'ID=u;Parent=t') + cds(('c1', 1, 6, '+')),
+        'two_mrna': g3h + cds(('c1', 1, 9, '+')) + _gff3('c1', 'mRNA', 1, 40, '-', 'ID=t2;Parent=g') +
+        _gff3('c1', 'CDS', 4, 30, '-', 'ID=c2;Parent=t2'),
+        'child_before_parent': _gff3('c1', 'CDS', 1, 6, '+', 'ID=c;Parent=t') + g3h,
+        'comment_lines': '#c\n' + g3h + '##x\n' + cds(('c1', 1, 12, '+')),
+        'gtf_two_genes': _gtf_line('c1', 1, 9, '+', 't1', 'g1') + _gtf_line('c1', 12, 20, '+', 't1', 'g1') +
+        _gtf_line('c2 desc', 1, 12, '-', 't2', 'g2'),
+        'gtf_gene_only': 'c1\tt\tCDS\t1\t9\t.\t-\t0\tgene_id "gA";\nc1\tt\tCDS\t20\t30\t.\t-\t0\tgene_id "gA";\n',
+        'exon_ignored': g3h + _gff3('c1', 'exon', 1, 40, '+', 'ID=e;Parent=t') + cds(('c1', 2, 13, '+')),
+    }
+    return cases
+
+
+EDGE_CALLS = [('nucleotide', False, False), ('protein', False, False), ('nucleotide', True, False),
+              ('nucleotide', False, True), ('protein', True, False)]
+
+
+def make_edges(ref):
+    out = []
+    for name, gff in sorted(edge_case_inputs().items()):
+        for seq_type, longest, genomic in EDGE_CALLS:
+            def run():
+                g = ref.Genome(EDGE_GENOME)
+                g.read_gff(gff)
+                return g.annotations.get_fasta('gene', seq_type=seq_type, longest=longest,
+                                               genomic=genomic)
+            r, e, so = call(run)
+            out.append({'case': name, 'fasta': EDGE_GENOME, 'gff': gff, 'seq_type': seq_type,
+                        'longest': longest, 'genomic': genomic, 'result': r, 'exc': e,
+                        'stdout': so})
+    return out
+
+
+# ---------------------------------------------------------------------------
+
+def ref_gff2fasta(ref, fasta, gff, seq_type='nucleotide', longest=False, genomic=False,
+                  order='insertion'):
+    def run():
+        g = ref.Genome(fasta)
+        g.read_gff(gff)
+        if order == 'py2':
+            keys = mo.py2_order_after_deepcopy(list(g.annotations.gene))
+            g.annotations.gene = {k: g.annotations.gene[k] for k in keys}
+        return g.annotations.get_fasta('gene', seq_type=seq_type, longest=longest,
+                                       genomic=genomic) + '\n'
+    return call(run)
+
+
+def digest(res, exc, so):
+    d = {'exc': exc, 'stdout_sha256': sha(so)}
+    if res is not None:
+        crc, size = goldlib.posix_cksum(res)
+        d.update({'cksum': '%d %d' % (crc, size), 'sha256': sha(res)})
+    return d
+
+
+def make_fixture_hashes(ref):
+    out = {}
+    fa = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
+    gff = goldlib.path('O.biroi_NCBIrefseq_gff3Subset.gff')
+    for seq_type in ('nucleotide', 'protein'):
+        for order in ('insertion', 'py2'):
+            out['obiroi/%s/%s' % (seq_type, order)] = digest(
+                *ref_gff2fasta(ref, fa, gff, seq_type, order=order))
+    out['obiroi/genomic/insertion'] = digest(*ref_gff2fasta(ref, fa, gff, genomic=True))
+    out['obiroi/longest/insertion'] = digest(*ref_gff2fasta(ref, fa, gff, longest=True))
+    c14 = goldlib.rebuild_c14()
+    for ann in ('StandardGTF.gtf', 'transcriptlessGTF.gtf', 'minimalGFF3.gff'):
+        for seq_type in ('nucleotide', 'protein'):
+            for order in ('insertion', 'py2'):
+                out['c14/%s/%s/%s' % (ann, seq_type, order)] = digest(
+                    *ref_gff2fasta(ref, c14, goldlib.path(ann), seq_type, order=order))
+    return out
+
+
+def make_synth(ref):
+    from magot_amd import synth
+    w = synth.make('small')
+    fa = w.fasta_text()
+    out = {'fasta_sha256': sha(fa)}
+    for fmt, text in (('gff3', w.gff3_text()), ('gtf', w.gtf_text())):
+        out['%s_sha256' % fmt] = sha(text)
+        for seq_type in ('nucleotide', 'protein'):
+            out['%s/%s' % (fmt, seq_type)] = digest(*ref_gff2fasta(ref, fa, text, seq_type))
+    return out
+
+
+def main():
+    ref = reference_module()
+    with open(os.path.join(HERE, 'kat.json'), 'w') as fh:
+        json.dump(make_kat(ref), fh, indent=0, sort_keys=True)
+    with open(os.path.join(HERE, 'edge_cases.json'), 'w') as fh:
+        json.dump(make_edges(ref), fh, indent=0, sort_keys=True)
+    with open(os.path.join(HERE, 'fixtures.json'), 'w') as fh:
+        json.dump(make_fixture_hashes(ref), fh, indent=1, sort_keys=True)
+    with open(os.path.join(HERE, 'synth_small.json'), 'w') as fh:
+        json.dump(make_synth(ref), fh, indent=1, sort_keys=True)
+    print('golden vectors written to', HERE)
+
+
+if __name__ == '__main__':
+    main()

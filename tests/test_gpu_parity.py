@@ -1,0 +1,293 @@
+"""Parity of the HIP path (through the C ABI) with the reference goldens and the
+CPU oracle.  Needs an MI355X: ``pytest -m gpu``."""
+
+import contextlib
+import hashlib
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+
+import goldlib
+from magot_amd import engine, synth
+from magot_amd import genome as G
+
+pytestmark = pytest.mark.gpu
+
+
+def _json(name):
+    with open(os.path.join(goldlib.HERE, name)) as fh:
+        return json.load(fh)
+
+
+def _sha(s):
+    if isinstance(s, str):
+        s = s.encode('latin-1')
+    return hashlib.sha256(s).hexdigest()
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _device():
+    from magot_amd import _lib
+    if _lib.lib().magot_device_count() <= 0:
+        pytest.fail('no HIP device visible for a gpu test')
+
+
+# ---------------------------------------------------------------------------
+# Sequence ops (genome.py:784-851) vs known-answer vectors from the reference
+# ---------------------------------------------------------------------------
+
+def test_revcomp_kat_batch():
+    recs = _json('kat.json')
+    got = engine.revcomp_batch([r['seq'] for r in recs])
+    assert got == [r['revcomp'] for r in recs]
+
+
+def test_translate_kat_batch():
+    recs = _json('kat.json')
+    seqs, frames, strands, want, trims = [], [], [], [], []
+    for r in recs:
+        for key, exp in r['translate'].items():
+            if isinstance(exp, dict):
+                continue
+            seqs.append(r['seq'])
+            frames.append(int(key[0]))
+            strands.append(key[1])
+            trims.append(bool(int(key[2])))
+            want.append(exp)
+    got = engine.translate_batch(seqs, frames, strands)
+    for s, f, st, t, g, w in zip(seqs, frames, strands, trims, got, want):
+        if g is not None and t and g[:1] == 'X':
+            g = g[1:]
+        assert g == w, (s, f, st, t)
+
+
+def test_sequence_api_kat():
+    S = G.Sequence('ATGGCCTTTAAACCCGGGTAG')
+    assert S.translate() == 'MAFKPG*'
+    assert S.translate(strand='-') == 'LPGFKGH'
+    assert S.translate(frame=1) == 'GL*TRV'
+    assert S.translate(frame=2, strand='-') == 'PGLKA'
+    assert G.Sequence('NNNATGNNN').translate() == 'MX'
+    assert G.Sequence('AT').translate() is None
+    assert G.Sequence('ATGC').translate(frame=1) == ''
+    assert G.Sequence('ACGTRYacgtn-*.').reverse_compliment() == 'nn-nacgtnnACGT'
+    assert isinstance(S.reverse_compliment(), G.Sequence)
+    for r in _json('kat.json')[:14]:
+        for key, exp in r['orfs'].items():
+            longest, atg = bool(int(key[0])), bool(int(key[1]))
+            if isinstance(exp, dict):
+                with pytest.raises(Exception) as ei:
+                    G.Sequence(r['seq']).get_orfs(longest=longest, from_atg=atg)
+                assert type(ei.value).__name__ == exp['exc']
+            else:
+                assert G.Sequence(r['seq']).get_orfs(longest=longest, from_atg=atg) == exp
+
+
+def test_custom_library():
+    lib = dict(G.Sequence._STANDARD)
+    lib['ATG'] = 'Z'
+    assert G.Sequence('ATGATG').translate(library=lib) == 'ZZ'
+
+
+# ---------------------------------------------------------------------------
+# get_fasta: edge cases, the reference's fixtures, its test-suite cksums
+# ---------------------------------------------------------------------------
+
+def test_edge_cases_gpu(capsys):
+    for case in _json('edge_cases.json'):
+        capsys.readouterr()
+        res = exc = None
+        try:
+            g = G.Genome(case['fasta'])
+            g.read_gff(case['gff'])
+            res = g.annotations.get_fasta('gene', seq_type=case['seq_type'],
+                                          longest=case['longest'], genomic=case['genomic'])
+        except Exception as e:  # noqa: BLE001
+            exc = type(e).__name__
+        out = capsys.readouterr().out
+        tag = (case['case'], case['seq_type'], case['longest'], case['genomic'])
+        assert exc == case['exc'], tag
+        assert res == case['result'], tag
+        assert out == case['stdout'], tag
+
+
+def test_get_seq_single_interval():
+    g = G.Genome('>c1\nACGTACGTAAccggttNNRYacgtACGTAAATTTGGGCCC\n')
+    g.read_gff('c1\tt\tgene\t1\t40\t.\t+\t.\tID=g\n'
+               'c1\tt\tmRNA\t1\t40\t.\t+\t.\tID=t;Parent=g\n'
+               'c1\tt\tCDS\t10\t20\t.\t-\t0\tID=c;Parent=t\n')
+    s = g.annotations.CDS['c'].get_seq()
+    assert s == 'nnNNaaccggT' and isinstance(s, G.Sequence)
+
+
+def _gff2fasta(fasta, gff, **kw):
+    order = kw.pop('order', 'insertion')
+    g = G.Genome(fasta)
+    g.read_gff(gff)
+    return g.annotations.get_fasta('gene', order=order, **kw) + '\n'
+
+
+@pytest.mark.parametrize('key', ['obiroi/nucleotide/insertion', 'obiroi/protein/insertion',
+                                 'obiroi/nucleotide/py2', 'obiroi/protein/py2',
+                                 'obiroi/longest/insertion', 'obiroi/genomic/insertion'])
+def test_obiroi_gpu(key):
+    want = _json('fixtures.json')[key]
+    _, kind, order = key.split('/')
+    kw = {'order': order}
+    if kind == 'protein':
+        kw['seq_type'] = 'protein'
+    if kind == 'longest':
+        kw['longest'] = True
+    if kind == 'genomic':
+        kw['genomic'] = True
+    buf = io.StringIO()
+    try:
+        with contextlib.redirect_stdout(buf):
+            out = _gff2fasta(goldlib.path('O.biroi_refseqGenomeSubset.fasta'),
+                             goldlib.path('O.biroi_NCBIrefseq_gff3Subset.gff'), **kw)
+        exc = None
+    except Exception as e:  # noqa: BLE001
+        out, exc = None, type(e).__name__
+    assert exc == want['exc']
+    assert _sha(buf.getvalue()) == want['stdout_sha256']
+    if out is not None:
+        assert _sha(out) == want['sha256']
+        crc, n = goldlib.posix_cksum(out)
+        assert '%d %d' % (crc, n) == want['cksum']
+
+
+@pytest.fixture(scope='module')
+def c14_path(tmp_path_factory):
+    p = tmp_path_factory.mktemp('c14') / 'C14.fasta'
+    p.write_bytes(goldlib.rebuild_c14().encode('latin-1'))
+    return str(p)
+
+
+@pytest.mark.parametrize('ann', ['StandardGTF.gtf', 'transcriptlessGTF.gtf', 'minimalGFF3.gff'])
+def test_c14_annotations_gpu(c14_path, ann):
+    table = _json('fixtures.json')
+    for seq_type in ('nucleotide', 'protein'):
+        for order in ('insertion', 'py2'):
+            out = _gff2fasta(c14_path, goldlib.path(ann), seq_type=seq_type, order=order)
+            assert _sha(out) == table['c14/%s/%s/%s' % (ann, seq_type, order)]['sha256'], \
+                (ann, seq_type, order)
+
+
+def _cli(argv):
+    from magot_amd import genome_tools
+
+    class _Out(object):
+        def __init__(self):
+            self.buffer = io.BytesIO()
+
+        def write(self, s):
+            self.buffer.write(s.encode('latin-1'))
+
+        def flush(self):
+            pass
+
+    out = _Out()
+    with contextlib.redirect_stdout(out):
+        genome_tools.main(argv)
+    return out.buffer.getvalue()
+
+
+def test_reference_test_suite_lines_12_13_14(c14_path):
+    """test_data/test_suite.py:12-14 through the drop-in CLI, byte for byte."""
+    data = _cli(['gff2fasta', c14_path, goldlib.path('StandardGTF.gtf')])
+    assert goldlib.posix_cksum(data) == (2836090577, 690750)
+    data = _cli(['gff2fasta', c14_path, goldlib.path('StandardGTF.gtf'), 'seq_type=protein'])
+    assert goldlib.posix_cksum(data) == (111942461, 233762)
+    data = _cli(['cds2pep', goldlib.path('CDSannotations.cds')])
+    assert goldlib.posix_cksum(data) == (111942461, 233762)
+
+
+def test_synth_small_gpu():
+    want = _json('synth_small.json')
+    w = synth.make('small')
+    fa = w.fasta_text()
+    for fmt, text in (('gff3', w.gff3_text()), ('gtf', w.gtf_text())):
+        for seq_type in ('nucleotide', 'protein'):
+            out = _gff2fasta(fa, text, seq_type=seq_type)
+            assert _sha(out) == want['%s/%s' % (fmt, seq_type)]['sha256'], (fmt, seq_type)
+
+
+# ---------------------------------------------------------------------------
+# Direct plan tables vs the C oracle (random shapes, ragged edges, full size)
+# ---------------------------------------------------------------------------
+
+def gpu_extract(w, outputs=engine.OUT_NUC | engine.OUT_PEP):
+    dev = engine.DeviceGenome(w.contigs())
+    ex, tx = w.plan_tables()
+    plan = engine.ExtractionPlan(dev, ex, tx, outputs)
+    nuc, noff, pep, poff = plan.run()
+    plan.close()
+    dev.close()
+    return nuc, noff, pep, poff
+
+
+def trimmed(pep, poff):
+    """Apply trimX (drop one leading 'X' per record) to the untrimmed output."""
+    starts = poff[:-1].astype(np.int64)
+    lens = (poff[1:] - poff[:-1]).astype(np.int64)
+    first = np.zeros(len(starts), dtype=bool)
+    nonempty = lens > 0
+    first[nonempty] = pep[starts[nonempty]] == ord('X')
+    keep = np.ones(len(pep), dtype=bool)
+    keep[starts[first]] = False
+    lens -= first
+    off = np.zeros(len(lens) + 1, dtype=np.int64)
+    np.cumsum(lens, out=off[1:])
+    return pep[keep], off
+
+
+def check_against_oracle(w):
+    from oracle import cds_oracle
+    nuc, noff, pep, poff = gpu_extract(w)
+    ref, roff, st = cds_oracle.extract_workload(w, False)
+    assert not st.any()
+    assert np.array_equal(noff.astype(np.int64), roff)
+    if not np.array_equal(nuc, ref):
+        bad = int(np.nonzero(nuc != ref)[0][0])
+        t = int(np.searchsorted(roff, bad, side='right') - 1)
+        raise AssertionError('nucleotide mismatch at byte %d (record %d): %r vs %r' % (
+            bad, t, nuc[max(0, bad - 8):bad + 8].tobytes(), ref[max(0, bad - 8):bad + 8].tobytes()))
+    pref, proff, pst = cds_oracle.extract_workload(w, True)
+    got, goff = trimmed(pep, poff)
+    ok = pst == 0
+    assert np.array_equal(goff[1:][ok] - goff[:-1][ok], proff[1:][ok] - proff[:-1][ok])
+    assert np.array_equal(got, pref)
+
+
+@pytest.mark.parametrize('seed', [1, 2, 3])
+def test_random_workloads_vs_c_oracle(seed):
+    w = synth.make('small', seed=seed, genome_bases=3_000_000, n_tx=1500, iupac_rate=1e-3)
+    check_against_oracle(w)
+
+
+def test_tiny_exons_and_lds_overflow_vs_c_oracle():
+    """1-12 base exons: many exons per 16-byte chunk and > 512 exons per tile
+    (the kernel's global-memory search path)."""
+    rng = np.random.default_rng(99)
+    w = synth.make('small', seed=5, genome_bases=400_000, n_tx=400, iupac_rate=5e-3)
+    w.ex_len = rng.integers(1, 13, size=w.n_exons).astype(np.int64)
+    check_against_oracle(w)
+
+
+def test_c2_shape_nucleotide_only():
+    from oracle import cds_oracle
+    w = synth.make('C2', genome_bases=20_000_000, n_tx=10_000)
+    nuc, noff, pep, poff = gpu_extract(w, engine.OUT_NUC)
+    ref, roff, st = cds_oracle.extract_workload(w, False)
+    assert pep is None
+    assert np.array_equal(nuc, ref)
+
+
+@pytest.mark.slow
+def test_c3_full_size_vs_c_oracle():
+    """The headline workload (1 Gb genome, 500k transcripts), byte for byte."""
+    w = synth.make('C3')
+    check_against_oracle(w)
