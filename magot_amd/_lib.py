@@ -44,7 +44,7 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 _vp = ctypes.c_void_p
 
 _lib = None
-_lib_lock = threading.Lock()
+_lib_lock = threading.RLock()
 
 
 def _declare(lib):
