@@ -219,9 +219,8 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   }
   *out = nullptr;
   const uint64_t E = n_exons, T = n_tx;
-  // --- host tables --------------------------------------------------------
-  std::vector<uint64_t> ex_g(E), ex_out(E + 1), tx_nuc(T + 1), tx_pep(T + 1);
-  uint64_t expect = 0, acc = 0;
+  // --- validate and build per-record offsets --------------------------------
+  uint64_t expect = 0;
   for (uint64_t t = 0; t < T; ++t) {
     if (txs[t].exon_begin != expect) {
       set_error("magot_plan_create: record " + std::to_string(t) +
@@ -239,67 +238,115 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     return MAGOT_ERR_ARG;
   }
   const uint64_t n_contigs = g->contig_base.size();
-  for (uint64_t e = 0; e < E; ++e) {
-    const magot_exon& x = exons[e];
-    const uint64_t st = x.start_rc & ~kRcBit;
-    if (x.contig >= n_contigs || st + x.len > g->contig_len[x.contig] ||
-        st > g->contig_len[x.contig]) {
-      set_error("magot_plan_create: exon " + std::to_string(e) + " outside its contig");
-      return MAGOT_ERR_RANGE;
-    }
-    ex_g[e] = (g->contig_base[x.contig] + st) | (x.start_rc & kRcBit);
-    ex_out[e] = acc;
-    acc += x.len;
-  }
-  ex_out[E] = acc;
-  const uint64_t B = acc;
-  uint64_t P = 0;
+  // Compacted interval table: zero-length intervals add no output.
+  std::vector<uint64_t> ex_g, ex_out;
+  ex_g.reserve(E);
+  ex_out.reserve(E + 1);
+  std::vector<uint64_t> nuc_off(T + 1), pep_off(T + 1);
+  uint64_t acc = 0, P = 0;
   for (uint64_t t = 0; t < T; ++t) {
-    tx_nuc[t] = ex_out[txs[t].exon_begin];
-    tx_pep[t] = P;
-    const uint64_t L = ex_out[txs[t].exon_begin + txs[t].n_exons] - tx_nuc[t];
-    P += L / 3;
+    nuc_off[t] = acc;
+    pep_off[t] = P;
+    const uint64_t e0 = txs[t].exon_begin, e1 = e0 + txs[t].n_exons;
+    for (uint64_t e = e0; e < e1; ++e) {
+      const magot_exon& x = exons[e];
+      const uint64_t st = x.start_rc & ~kRcBit;
+      if (x.contig >= n_contigs || st > g->contig_len[x.contig] ||
+          st + x.len > g->contig_len[x.contig]) {
+        set_error("magot_plan_create: exon " + std::to_string(e) + " outside its contig");
+        return MAGOT_ERR_RANGE;
+      }
+      if (x.len == 0) continue;
+      ex_g.push_back((g->contig_base[x.contig] + st) | (x.start_rc & kRcBit));
+      ex_out.push_back(acc);
+      acc += x.len;
+    }
+    P += (acc - nuc_off[t]) / 3;
   }
-  tx_nuc[T] = B;
-  tx_pep[T] = P;
+  nuc_off[T] = acc;
+  pep_off[T] = P;
+  const uint64_t B = acc;
+  const uint64_t Ec = ex_g.size();
+  ex_out.push_back(B);
+  // Compacted record table: records with at least one codon.
+  std::vector<uint64_t> tn, tp;
+  for (uint64_t t = 0; t < T; ++t)
+    if (pep_off[t + 1] > pep_off[t]) {
+      tn.push_back(nuc_off[t]);
+      tp.push_back(pep_off[t]);
+    }
+  const uint64_t Tc = tn.size();
+  tn.push_back(B);
+  tp.push_back(P);
+  if (Ec >= 0xFFFFFFFFull || Tc >= 0xFFFFFFFFull) {
+    set_error("magot_plan_create: table too large for one plan (split it)");
+    return MAGOT_ERR_ARG;
+  }
 
-  const uint64_t n_tiles64 = (B + kTile - 1) / kTile;
+  // --- tiles ----------------------------------------------------------------
+  // residues whose codon starts before output byte T (monotone pointer jq)
+  uint64_t jq = 0;
+  auto pcount = [&](uint64_t T) -> uint64_t {
+    while (jq < Tc && tn[jq + 1] <= T) ++jq;
+    if (jq >= Tc) return P;
+    if (tn[jq] > T) return tp[jq];                           // before the first record
+    const uint64_t into = T - tn[jq];
+    return tp[jq] + std::min((into + 2) / 3, tp[jq + 1] - tp[jq]);
+  };
+  std::vector<uint64_t> tile_start, tile_q;
+  std::vector<uint32_t> tile_ex, tile_tx;
+  uint64_t e1 = 0, e2 = 0, j1 = 0, j2 = 0;
+  uint64_t T0 = 0;
+  uint64_t Q0 = pcount(0);
+  while (T0 < B) {
+    while (e1 < Ec && ex_out[e1 + 1] <= T0) ++e1;           // interval containing T0
+    while (j1 < Tc && tp[j1 + 1] <= Q0) ++j1;               // record holding residue Q0
+    uint64_t T1 = std::min<uint64_t>(T0 + kTile, B);
+    if (e1 + kExonCap < Ec) T1 = std::min<uint64_t>(T1, ex_out[e1 + kExonCap] - kHalo);
+    if (j1 + kTxCap < Tc) T1 = std::min<uint64_t>(T1, tn[j1 + kTxCap]);
+    if (T1 < B) T1 &= ~(uint64_t)(kChunk - 1);
+    if (T1 < T0 + kChunk) T1 = std::min<uint64_t>(T0 + kChunk, B);
+    const uint64_t Q1 = pcount(T1);
+    const uint64_t dec_end = std::min<uint64_t>(T1 + kHalo, B);
+    if (e2 < e1) e2 = e1;
+    while (e2 < Ec && ex_out[e2] < dec_end) ++e2;           // intervals touching the decode range
+    if (j2 < j1) j2 = j1;
+    while (j2 < Tc && tp[j2] < Q1) ++j2;                    // records holding residues [Q0, Q1)
+    if (e2 - e1 > (uint64_t)kExonCap || (Q1 > Q0 && j2 - j1 > (uint64_t)kTxCap)) {
+      set_error("magot_plan_create: internal tiling error");
+      return MAGOT_ERR_STATE;
+    }
+    tile_start.push_back(T0);
+    tile_q.push_back(Q0);
+    tile_ex.push_back((uint32_t)e1);
+    tile_ex.push_back((uint32_t)e2);
+    tile_tx.push_back((uint32_t)j1);
+    tile_tx.push_back((uint32_t)(Q1 > Q0 ? j2 : j1));
+    T0 = T1;
+    Q0 = Q1;
+  }
+  tile_start.push_back(B);
+  tile_q.push_back(P);
+  const uint64_t n_tiles64 = tile_start.size() - 1;
   if (n_tiles64 >= 0x7FFFFFFFull) {
     set_error("magot_plan_create: output too large for one launch");
     return MAGOT_ERR_ARG;
   }
   const uint32_t n_tiles = (uint32_t)n_tiles64;
-  std::vector<uint32_t> tile_ex(2 * (uint64_t)n_tiles + 2), tile_t(n_tiles + 1);
-  std::vector<uint64_t> tile_q(n_tiles + 1);
-  uint64_t e1 = 0, e2 = 0, tt = 0;
-  for (uint32_t k = 0; k < n_tiles; ++k) {
-    const uint64_t T0 = (uint64_t)k * kTile;
-    while (e1 < E && ex_out[e1 + 1] <= T0) ++e1;           // exon containing T0
-    const uint64_t lim = T0 + kTile + kHalo;
-    if (e2 < e1) e2 = e1;
-    while (e2 < E && ex_out[e2] < lim) ++e2;              // first exon starting past the halo
-    tile_ex[2 * k] = (uint32_t)e1;
-    tile_ex[2 * k + 1] = (uint32_t)e2;
-    while (tt < T && tx_nuc[tt + 1] <= T0) ++tt;           // record containing T0
-    tile_t[k] = (uint32_t)tt;
-    const uint64_t into = T0 - tx_nuc[tt];
-    tile_q[k] = tx_pep[tt] + std::min((into + 2) / 3, tx_pep[tt + 1] - tx_pep[tt]);
-  }
-  tile_t[n_tiles] = T ? (uint32_t)(T - 1) : 0;
-  tile_q[n_tiles] = P;
 
-  // --- device arena ---------------------------------------------------------
+  // --- device arena -----------------------------------------------------------
   std::unique_ptr<magot_plan> p(new magot_plan());
   p->ctx = ctx;
   p->g = g;
   Carve cv;
-  const uint64_t o_exg = cv.take<uint64_t>(E + 1);
-  const uint64_t o_exo = cv.take<uint64_t>(E + 1);
-  const uint64_t o_txn = cv.take<uint64_t>(T + 1);
-  const uint64_t o_txp = cv.take<uint64_t>(T + 1);
-  const uint64_t o_tex = cv.take<uint32_t>(tile_ex.size());
+  const uint64_t o_exg = cv.take<uint64_t>(Ec + 1);
+  const uint64_t o_exo = cv.take<uint64_t>(Ec + 1);
+  const uint64_t o_txn = cv.take<uint64_t>(Tc + 1);
+  const uint64_t o_txp = cv.take<uint64_t>(Tc + 1);
+  const uint64_t o_ts = cv.take<uint64_t>(tile_start.size());
+  const uint64_t o_tex = cv.take<uint32_t>(tile_ex.size() + 2);
+  const uint64_t o_ttx = cv.take<uint32_t>(tile_tx.size() + 2);
   const uint64_t o_tq = cv.take<uint64_t>(tile_q.size());
-  const uint64_t o_tt = cv.take<uint32_t>(tile_t.size());
   const uint64_t o_nuc = cv.take<uint8_t>((outputs & MAGOT_OUT_NUC) ? B + 64 : 64);
   const uint64_t o_pep = cv.take<uint8_t>((outputs & MAGOT_OUT_PEP) ? P + 64 : 64);
   MAGOT_HIP_TRY(hipMalloc(&p->arena, cv.used));
@@ -309,13 +356,14 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     if (!bytes) return hipSuccess;
     return hipMemcpy(base + off, src, bytes, hipMemcpyHostToDevice);
   };
-  MAGOT_HIP_TRY(up(o_exg, ex_g.data(), E * 8));
-  MAGOT_HIP_TRY(up(o_exo, ex_out.data(), (E + 1) * 8));
-  MAGOT_HIP_TRY(up(o_txn, tx_nuc.data(), (T + 1) * 8));
-  MAGOT_HIP_TRY(up(o_txp, tx_pep.data(), (T + 1) * 8));
+  MAGOT_HIP_TRY(up(o_exg, ex_g.data(), Ec * 8));
+  MAGOT_HIP_TRY(up(o_exo, ex_out.data(), (Ec + 1) * 8));
+  MAGOT_HIP_TRY(up(o_txn, tn.data(), (Tc + 1) * 8));
+  MAGOT_HIP_TRY(up(o_txp, tp.data(), (Tc + 1) * 8));
+  MAGOT_HIP_TRY(up(o_ts, tile_start.data(), tile_start.size() * 8));
   MAGOT_HIP_TRY(up(o_tex, tile_ex.data(), tile_ex.size() * 4));
+  MAGOT_HIP_TRY(up(o_ttx, tile_tx.data(), tile_tx.size() * 4));
   MAGOT_HIP_TRY(up(o_tq, tile_q.data(), tile_q.size() * 8));
-  MAGOT_HIP_TRY(up(o_tt, tile_t.data(), tile_t.size() * 4));
 
   ExtractArgs& a = p->args;
   a.codes = g->codes;
@@ -326,9 +374,10 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   a.ex_out = reinterpret_cast<const uint64_t*>(base + o_exo);
   a.tx_nuc = reinterpret_cast<const uint64_t*>(base + o_txn);
   a.tx_pep = reinterpret_cast<const uint64_t*>(base + o_txp);
+  a.tile_start = reinterpret_cast<const uint64_t*>(base + o_ts);
   a.tile_ex = reinterpret_cast<const uint32_t*>(base + o_tex);
+  a.tile_tx = reinterpret_cast<const uint32_t*>(base + o_ttx);
   a.tile_q = reinterpret_cast<const uint64_t*>(base + o_tq);
-  a.tile_t = reinterpret_cast<const uint32_t*>(base + o_tt);
   a.nuc = reinterpret_cast<uint8_t*>(base + o_nuc);
   a.pep = reinterpret_cast<uint8_t*>(base + o_pep);
   a.total_nuc = B;
@@ -339,8 +388,8 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   standard_lut(lut);
   std::memcpy(a.lut, lut, 64);
 
-  p->nuc_off = std::move(tx_nuc);
-  p->pep_off = std::move(tx_pep);
+  p->nuc_off = std::move(nuc_off);
+  p->pep_off = std::move(pep_off);
   p->n_exons = E;
   p->n_tx = T;
   if (nuc_bytes) *nuc_bytes = B;

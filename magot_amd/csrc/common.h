@@ -53,20 +53,26 @@ constexpr int kChunksPerThread = 3;
 constexpr int kTile = kThreads * kChunk * kChunksPerThread;   // 12288 nucleotide bytes
 constexpr int kHalo = kChunk;                 // codons may run 2 bytes past the tile
 constexpr int kTileChunks = kTile / kChunk;   // 768
-constexpr int kExonCap = 512;                 // exons cached in LDS per tile
+constexpr int kExonCap = 512;                 // intervals staged in LDS per tile
+constexpr int kTxCap = 256;                   // records staged in LDS per tile
 
+// Device plan.  Zero-length intervals and records without a codon are
+// compacted away on the host (they add no output); tiles are 16-byte aligned
+// ranges of the nucleotide output of at most kTile bytes, cut shorter where
+// they would touch more than kExonCap intervals or kTxCap records.
 struct ExtractArgs {
   const uint32_t* codes;
   const uint32_t* lower;
   const ExcRun* runs;
   const uint32_t* dir;
-  const uint64_t* ex_g;       // per exon: global start | kRcBit
-  const uint64_t* ex_out;     // n_exons+1 output prefix offsets
-  const uint64_t* tx_nuc;     // n_tx+1
-  const uint64_t* tx_pep;     // n_tx+1
-  const uint32_t* tile_ex;    // 2 per tile: [first exon, end exon)
-  const uint64_t* tile_q;     // n_tiles+1: first residue produced by the tile
-  const uint32_t* tile_t;     // n_tiles+1: record containing the tile start
+  const uint64_t* ex_g;       // per interval: global genome start | kRcBit
+  const uint64_t* ex_out;     // n+1 output prefix offsets
+  const uint64_t* tx_nuc;     // per codon-bearing record: output start (n+1, sentinel B)
+  const uint64_t* tx_pep;     // per codon-bearing record: residue start (n+1, sentinel P)
+  const uint64_t* tile_start; // n_tiles+1
+  const uint32_t* tile_ex;    // 2 per tile: [first interval, end)
+  const uint32_t* tile_tx;    // 2 per tile: [first record, end)
+  const uint64_t* tile_q;     // n_tiles+1: first residue whose codon starts in the tile
   uint8_t* nuc;
   uint8_t* pep;
   uint64_t total_nuc;
