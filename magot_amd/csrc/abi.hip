@@ -1,6 +1,7 @@
 // C ABI of libmagot.so (declarations and contracts: include/magot.h).
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
@@ -33,6 +34,8 @@ using namespace magot;
 
 struct magot_ctx {
   int device = 0;
+  int n_cu = 0;
+  int blocks_per_cu = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 };
@@ -46,6 +49,8 @@ struct magot_genome {
   ExcRun* runs = nullptr;
   uint32_t* dir = nullptr;
   std::vector<uint64_t> contig_base, contig_len;
+  std::vector<ExcRun> host_runs;   // host copies for per-interval exception flags
+  std::vector<uint32_t> host_dir;
   uint64_t extent = 0, total_bases = 0, n_runs = 0;
 };
 
@@ -115,6 +120,8 @@ int magot_ctx_create(int device, magot_ctx** out) {
   MAGOT_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   MAGOT_HIP_TRY(hipEventCreate(&c->ev0));
   MAGOT_HIP_TRY(hipEventCreate(&c->ev1));
+  MAGOT_HIP_TRY(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
+  c->blocks_per_cu = extract_blocks_per_cu();
   *out = c.release();
   return MAGOT_OK;
 }
@@ -175,9 +182,11 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
   MAGOT_HIP_TRY(hipMemcpy(g->dir, hp.dir.data(), hp.dir.size() * 4, hipMemcpyHostToDevice));
   g->contig_base = std::move(hp.contig_base);
   g->contig_len = std::move(hp.contig_len);
+  g->n_runs = hp.runs.size() - 1;
+  g->host_runs = std::move(hp.runs);
+  g->host_dir = std::move(hp.dir);
   g->extent = hp.extent;
   g->total_bases = hp.extent - kOrigin;
-  g->n_runs = hp.runs.size() - 1;
   *out = g.release();
   return MAGOT_OK;
 }
@@ -257,7 +266,12 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
         return MAGOT_ERR_RANGE;
       }
       if (x.len == 0) continue;
-      ex_g.push_back((g->contig_base[x.contig] + st) | (x.start_rc & kRcBit));
+      const uint64_t gs = g->contig_base[x.contig] + st;
+      // does [gs, gs+len) touch an exception run?  (dir: first run ending past the block)
+      uint64_t d = g->host_dir[gs >> kDirShift] & ~kDirClean;
+      while (g->host_runs[d].start + g->host_runs[d].len <= gs) ++d;
+      const uint64_t exc = g->host_runs[d].start < gs + x.len ? kExcBit : 0;
+      ex_g.push_back(gs | (x.start_rc & kRcBit) | exc);
       ex_out.push_back(acc);
       acc += x.len;
     }
@@ -339,10 +353,15 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   p->ctx = ctx;
   p->g = g;
   Carve cv;
+  // one padding row past each table: the kernel prefetches clamped rows j <= n
+  ex_g.push_back(0);
+  ex_out.push_back(B);
+  tn.push_back(B);
+  tp.push_back(P);
   const uint64_t o_exg = cv.take<uint64_t>(Ec + 1);
-  const uint64_t o_exo = cv.take<uint64_t>(Ec + 1);
-  const uint64_t o_txn = cv.take<uint64_t>(Tc + 1);
-  const uint64_t o_txp = cv.take<uint64_t>(Tc + 1);
+  const uint64_t o_exo = cv.take<uint64_t>(Ec + 2);
+  const uint64_t o_txn = cv.take<uint64_t>(Tc + 2);
+  const uint64_t o_txp = cv.take<uint64_t>(Tc + 2);
   const uint64_t o_ts = cv.take<uint64_t>(tile_start.size());
   const uint64_t o_tex = cv.take<uint32_t>(tile_ex.size() + 2);
   const uint64_t o_ttx = cv.take<uint32_t>(tile_tx.size() + 2);
@@ -356,10 +375,10 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     if (!bytes) return hipSuccess;
     return hipMemcpy(base + off, src, bytes, hipMemcpyHostToDevice);
   };
-  MAGOT_HIP_TRY(up(o_exg, ex_g.data(), Ec * 8));
-  MAGOT_HIP_TRY(up(o_exo, ex_out.data(), (Ec + 1) * 8));
-  MAGOT_HIP_TRY(up(o_txn, tn.data(), (Tc + 1) * 8));
-  MAGOT_HIP_TRY(up(o_txp, tp.data(), (Tc + 1) * 8));
+  MAGOT_HIP_TRY(up(o_exg, ex_g.data(), (Ec + 1) * 8));
+  MAGOT_HIP_TRY(up(o_exo, ex_out.data(), (Ec + 2) * 8));
+  MAGOT_HIP_TRY(up(o_txn, tn.data(), (Tc + 2) * 8));
+  MAGOT_HIP_TRY(up(o_txp, tp.data(), (Tc + 2) * 8));
   MAGOT_HIP_TRY(up(o_ts, tile_start.data(), tile_start.size() * 8));
   MAGOT_HIP_TRY(up(o_tex, tile_ex.data(), tile_ex.size() * 4));
   MAGOT_HIP_TRY(up(o_ttx, tile_tx.data(), tile_tx.size() * 4));
@@ -384,6 +403,15 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   a.total_pep = P;
   a.n_tiles = n_tiles;
   a.outputs = outputs;
+  a.grid = (uint32_t)(ctx->n_cu > 0 && ctx->blocks_per_cu > 0 ? ctx->n_cu * ctx->blocks_per_cu : 0);
+  if (const char* gb = std::getenv("MAGOT_GRID_BLOCKS")) a.grid = (uint32_t)std::atoi(gb);
+  if (const char* dbg = std::getenv("MAGOT_DEBUG_PATHS")) {
+    const int v = std::atoi(dbg);
+    if (v & 1) a.outputs |= kDebugSlowNuc;
+    if (v & 2) a.outputs |= kDebugSlowPep;
+    if (v & 4) a.outputs |= kDebugNoLoads;
+    if (v & 8) a.outputs |= kDebugPrologueOnly;
+  }
   uint8_t lut[64];
   standard_lut(lut);
   std::memcpy(a.lut, lut, 64);

@@ -47,14 +47,25 @@ void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, H
 // ---------------------------------------------------------------------------
 // Extraction tiling
 // ---------------------------------------------------------------------------
-constexpr int kThreads = 256;                 // one workgroup = 4 waves
+constexpr int kThreads = 256;                 // one workgroup = 4 independent waves
+constexpr int kWaves = kThreads / 64;
 constexpr int kChunk = 16;                    // bytes per lane-store
-constexpr int kChunksPerThread = 3;
-constexpr int kTile = kThreads * kChunk * kChunksPerThread;   // 12288 nucleotide bytes
+constexpr int kLaneChunks = 3;                // chunk slots per lane per tile
+constexpr int kSlots = 64 * kLaneChunks;      // 192 chunk slots per wave tile
+constexpr int kTile = 189 * kChunk;           // 3024 output bytes per tile: <= 1008 residues,
+                                              // so <= 64 residue chunks (one per lane)
 constexpr int kHalo = kChunk;                 // codons may run 2 bytes past the tile
-constexpr int kTileChunks = kTile / kChunk;   // 768
-constexpr int kExonCap = 512;                 // intervals staged in LDS per tile
-constexpr int kTxCap = 256;                   // records staged in LDS per tile
+constexpr int kExonCap = 128;                 // intervals staged in LDS per tile
+constexpr int kTxCap = 64;                    // records staged in LDS per tile
+constexpr int kPepSlots = 64;                 // residue chunks per tile
+constexpr uint64_t kExcBit = 1ull << 62;      // interval touches an exception run
+
+// Debug switches carried in ExtractArgs.outputs (env MAGOT_DEBUG_PATHS):
+// force the general per-segment / per-residue paths.
+constexpr uint32_t kDebugSlowNuc = 1u << 8;
+constexpr uint32_t kDebugSlowPep = 1u << 9;
+constexpr uint32_t kDebugNoLoads = 1u << 10;     // timing only: skip genome plane loads
+constexpr uint32_t kDebugPrologueOnly = 1u << 11;  // timing only: stop after staging
 
 // Device plan.  Zero-length intervals and records without a codon are
 // compacted away on the host (they add no output); tiles are 16-byte aligned
@@ -79,10 +90,12 @@ struct ExtractArgs {
   uint64_t total_pep;
   uint32_t n_tiles;
   uint32_t outputs;
+  uint32_t grid;              // persistent workgroups launched
   uint32_t lut[16];           // 64 residue bytes indexed c0 + 4*c1 + 16*c2
 };
 
 void launch_extract(const ExtractArgs& a, hipStream_t s);
+int extract_blocks_per_cu();
 
 // ---------------------------------------------------------------------------
 // Raw sequence batch ops (seqops.hip)

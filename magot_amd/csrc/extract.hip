@@ -11,36 +11,45 @@
 // moves bytes.
 //
 // Work decomposition (output-stationary, HBM-bound):
-//   * The concatenated nucleotide output of all records is cut by the host
-//     planner into tiles of <= 12 KiB (16-byte aligned; shorter only where a
-//     tile would hold more than kExonCap intervals or kTxCap records), one
-//     256-thread workgroup per tile.  Every lane owns 16-byte aligned output
-//     chunks, so every nucleotide store is one 16-byte global_store whatever
-//     the record or interval boundaries.
-//   * Prologue: the tile's intervals and records are staged in LDS, each as a
-//     32-bit tile-relative boundary plus a 64-bit genome "anchor" (genome
-//     coordinate of tile byte 0 along that interval, +p forward / -p reverse),
-//     and every chunk / residue chunk is told its interval / record by a
-//     scatter over boundaries -- no per-lane search.
-//   * A chunk inside one interval reads one 16-base window of the 2-bit code
-//     plane and of the soft-mask plane (two dword loads each; all three of a
-//     lane's chunks are issued before any is consumed), reverses it
-//     in-register for '-' intervals (bit-reverse, pair swap, complement),
-//     becomes ASCII with one v_perm per 4 bytes, and is patched from the
-//     exception run list only where the 4096-base directory flags a run.
-//     Chunks that cross an interval boundary take a per-segment loop.
-//   * The tile's codes and validity bits stay in LDS; a residue chunk (16
-//     residues of one record) funnel-shifts 48 bases of codes out of LDS,
-//     looks the 16 codons up in an LDS table and stores 16 bytes.  Ragged
-//     residue chunks (record boundary inside, tile edges) take a per-residue
-//     path.  Residue chunks of a tile are contiguous in the output.
+//   * The host cuts the concatenated nucleotide output into 16-byte aligned
+//     tiles of <= 3056 bytes (191 chunks of 16 bytes; shorter where a tile
+//     would touch more than kExonCap intervals or kTxCap records).  A tile
+//     belongs to ONE wavefront: 64 lanes x 3 chunk slots = 191 output chunks
+//     + 1 halo chunk (codons may run 2 bytes past the tile), so there are no
+//     workgroup barriers; waves are persistent and prefetch the next tile's
+//     descriptors and interval/record rows while the current tile computes.
+//   * Staging: the tile's intervals go to wave-private LDS as {64-bit genome
+//     anchor, tile-relative end, flags}; chunk -> interval and residue chunk
+//     -> record maps come from an LDS histogram + wave prefix scan.
+//   * A chunk is at most two interval segments on the fast path: each is a
+//     16-base window of the 2-bit code plane and the soft-mask plane (one
+//     dwordx2 load each), reversed in-register for '-' intervals (bit reverse,
+//     pair swap, complement), merged by mask, turned into ASCII with one
+//     v_perm per 4 bytes, and stored with one 16-byte store.  Intervals that
+//     touch an exception run (N, IUPAC ...; flagged per interval by the host)
+//     and chunks over 3+ intervals take a per-segment path.
+//   * Codes and validity bits stay in LDS; a residue chunk funnel-shifts 48
+//     bases of codes out of LDS per record segment (<= 2 on the fast path),
+//     looks the 16 codons up in an LDS table and stores 16 bytes.
 #include "common.h"
 
 namespace magot {
 namespace {
 
-constexpr int kPepChunks = kTile / 3 / 16 + 2;
-constexpr int kLdsChunks = kTileChunks + 4;
+constexpr int kGuard = 4;  // LDS words before codes[0] (codons of residue chunk 0 may start < 0)
+
+struct WaveLds {
+  uint4 ex[kExonCap];                     // {anchor lo, anchor hi, end (tile-rel), flags}
+  int64_t tn[kTxCap + 1];                 // record codon-0 output position, tile-relative
+  int64_t tp[kTxCap + 1];                 // record first residue, relative to the tile's Q0
+  uint32_t codes_g[kGuard + kSlots + 8];  // 2-bit codes per chunk (histogram scratch first)
+  uint32_t valid_g[kGuard + kSlots / 2 + 8];  // 16 validity bits per chunk (scratch first)
+  uint8_t cmap[kSlots];                   // chunk slot -> interval
+  uint8_t pmap[kPepSlots];                // residue chunk -> record
+};
+
+constexpr uint32_t kFlagRc = 1u;
+constexpr uint32_t kFlagExc = 2u;
 
 __device__ __forceinline__ uint32_t rev_pairs(uint32_t x) {
   // reverse the order of the sixteen 2-bit fields of x
@@ -48,23 +57,25 @@ __device__ __forceinline__ uint32_t rev_pairs(uint32_t x) {
   return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
 }
 
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbit(hi, lo, sh);  // (hi:lo >> sh)[31:0], sh in 0..31
+}
+
 __device__ __forceinline__ uint32_t spread_codes(uint32_t c8) {
   // four 2-bit codes -> four bytes 0..3
-  return (c8 | (c8 << 6) | (c8 << 12) | (c8 << 18)) & 0x03030303u;
+  const uint32_t x = c8 | (c8 << 6);
+  return (x | (x << 12)) & 0x03030303u;
 }
 
 __device__ __forceinline__ uint32_t spread_bits(uint32_t m4) {
   // four bits -> four bytes 0/1
-  return (m4 | (m4 << 7) | (m4 << 14) | (m4 << 21)) & 0x01010101u;
+  const uint32_t x = m4 | (m4 << 7);
+  return (x | (x << 14)) & 0x01010101u;
 }
 
 __device__ __forceinline__ uint32_t rc_literal(uint32_t b) {
   // genome.py:787,792 for a byte that is not ACGTacgt
   return (b == 'n' || b == 'N' || b == '-') ? b : (uint32_t)'n';
-}
-
-__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
-  return __builtin_amdgcn_alignbit(hi, lo, sh);  // (hi:lo >> sh)[31:0], sh in 0..31
 }
 
 struct Chunk {
@@ -78,34 +89,61 @@ __device__ __forceinline__ void put_literal(Chunk& o, int ka, int kb, uint32_t b
   const uint32_t n = (uint32_t)(kb - ka + 1);
   const uint32_t bits = ((n >= 32u) ? 0xFFFFFFFFu : ((1u << n) - 1u)) << ka;
   o.exc |= bits;
-  const uint32_t rep = byte * 0x01010101u;
+  const uint32_t rep = byte | (byte << 8) | (byte << 16) | (byte << 24);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t bm = spread_bits((bits >> (4 * q)) & 0xFu) * 0xFFu;
+    const uint32_t b01 = spread_bits((bits >> (4 * q)) & 0xFu);
+    const uint32_t bm = (b01 << 8) - b01;
     o.lit[q] = (o.lit[q] & ~bm) | (rep & bm);
   }
 }
 
-__device__ __forceinline__ uint4 chunk_ascii(const Chunk& o) {
+// 16 bytes of ASCII: 'ACGT' for codes 0..3, lower-case where the soft-mask
+// bit is set (selector bit 2 picks the 'acgt' source), literal bytes patched.
+__device__ __forceinline__ uint4 chunk_ascii(uint32_t codes, uint32_t low, uint32_t exc,
+                                             const uint32_t lit[4]) {
   uint32_t w[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const uint32_t sel = spread_codes((o.codes >> (8 * q)) & 0xFFu);
-    // bytes 'A','C','G','T' in both perm sources: selector 0..3 picks one.
-    uint32_t asc = __builtin_amdgcn_perm(0x54474341u, 0x54474341u, sel);
-    asc |= spread_bits((o.low >> (4 * q)) & 0xFu) << 5;
-    const uint32_t em = spread_bits((o.exc >> (4 * q)) & 0xFu) * 0xFFu;
-    w[q] = (asc & ~em) | (o.lit[q] & em);
+    const uint32_t sel = spread_codes((codes >> (8 * q)) & 0xFFu) |
+                         (spread_bits((low >> (4 * q)) & 0xFu) << 2);
+    w[q] = __builtin_amdgcn_perm(0x74676361u, 0x54474341u, sel);
+  }
+  if (exc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t b01 = spread_bits((exc >> (4 * q)) & 0xFu);
+      const uint32_t em = (b01 << 8) - b01;
+      w[q] = (w[q] & ~em) | (lit[q] & em);
+    }
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// Patch literal bytes (exception runs) of genome interval [glo, ghi] that maps
-// to chunk bytes starting at j0 (forward) or ending at j0 (reverse).
-__device__ __noinline__ Chunk patch_runs(const ExcRun* __restrict__ runs, uint32_t d, uint64_t glo,
-                                         uint64_t ghi, bool rc, int j0, Chunk o) {
-  for (;;) {
-    const ExcRun r = runs[d];
+struct Planes {
+  const uint32_t* __restrict__ codes;
+  const uint32_t* __restrict__ lower;
+  const uint32_t* __restrict__ dir;
+  const ExcRun* __restrict__ runs;
+};
+
+// Codes / soft-mask bits of the 16 genome bases starting at wbase.
+__device__ __forceinline__ void window(const Planes& a, uint64_t wbase, uint32_t& t,
+                                       uint32_t& lt) {
+  const uint2 c = *reinterpret_cast<const uint2*>(a.codes + (wbase >> 4));
+  const uint2 l = *reinterpret_cast<const uint2*>(a.lower + (wbase >> 5));
+  t = funnel(c.y, c.x, (uint32_t)(2 * (wbase & 15)));
+  lt = funnel(l.y, l.x, (uint32_t)(wbase & 31)) & 0xFFFFu;
+}
+
+// Patch literal bytes of genome interval [glo, ghi] (chunk bytes from j0).
+__device__ __forceinline__ void patch_runs(const Planes& a, uint64_t glo, uint64_t ghi, bool rc,
+                                           int j0, Chunk& o) {
+  const uint32_t d0 = a.dir[glo >> kDirShift];
+  const uint32_t d1 = a.dir[ghi >> kDirShift];
+  if ((d0 & kDirClean) && (d1 & kDirClean)) return;
+  for (uint32_t d = d0 & ~kDirClean;; ++d) {
+    const ExcRun r = a.runs[d];
     if (r.start > ghi) break;
     const uint64_t rend = r.start + r.len;
     if (rend > glo) {
@@ -114,33 +152,12 @@ __device__ __noinline__ Chunk patch_runs(const ExcRun* __restrict__ runs, uint32
       if (!rc) put_literal(o, j0 + (int)(ovl - glo), j0 + (int)(ovh - glo), r.byte);
       else put_literal(o, j0 + (int)(ghi - ovh), j0 + (int)(ghi - ovl), rc_literal(r.byte));
     }
-    ++d;
   }
-  return o;
 }
 
-// Codes / soft-mask bits of the 16 genome bases starting at wbase.
-struct Planes {
-  const uint32_t* __restrict__ codes;
-  const uint32_t* __restrict__ lower;
-  const uint32_t* __restrict__ dir;
-  const ExcRun* __restrict__ runs;
-};
-
-__device__ __forceinline__ void window(const Planes& a, uint64_t wbase, uint32_t& t,
-                                       uint32_t& lt) {
-  const uint64_t ci = wbase >> 4;
-  const uint32_t c0 = a.codes[ci], c1 = a.codes[ci + 1];
-  const uint64_t li = wbase >> 5;
-  const uint32_t l0 = a.lower[li], l1 = a.lower[li + 1];
-  t = funnel(c1, c0, (uint32_t)(2 * (wbase & 15)));
-  lt = funnel(l1, l0, (uint32_t)(wbase & 31)) & 0xFFFFu;
-}
-
-// General chunk assembly: any number of interval segments.
+// General chunk assembly: any number of interval segments, exception runs.
 __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
-                                               const int32_t* s_es, const uint64_t* s_anchor,
-                                               const uint8_t* s_rc) {
+                                               const uint4* ex) {
   Chunk o;
   o.codes = 0;
   o.low = 0;
@@ -149,11 +166,12 @@ __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
   const int end = min(p + kChunk, lim);
   int pos = p;
   while (pos < end) {
-    while (s_es[i + 1] <= pos) ++i;
+    uint4 X = ex[i];
+    while ((int)X.z <= pos) X = ex[++i];
     const int j0 = pos - p;
-    const int n = min(s_es[i + 1], end) - pos;
-    const uint64_t A = s_anchor[i];
-    const bool rc = s_rc[i] != 0;
+    const int n = min((int)X.z, end) - pos;
+    const uint64_t A = (uint64_t)X.x | ((uint64_t)X.y << 32);
+    const bool rc = (X.w & kFlagRc) != 0;
     uint64_t glo, ghi, wbase;
     if (!rc) {
       glo = A + (uint64_t)pos;
@@ -173,199 +191,347 @@ __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
     const uint32_t m2 = (n >= 16 ? 0xFFFFFFFFu : ((1u << (2 * n)) - 1u)) << (2 * j0);
     o.codes |= (t << (2 * j0)) & m2;
     o.low |= (lt << j0) & (((1u << n) - 1u) << j0);
-    const uint32_t d0 = a.dir[glo >> kDirShift];
-    const uint32_t d1 = a.dir[ghi >> kDirShift];
-    if (!((d0 & kDirClean) && (d1 & kDirClean)))
-      o = patch_runs(a.runs, d0 & ~kDirClean, glo, ghi, rc, j0, o);
+    if (X.w & kFlagExc) patch_runs(a, glo, ghi, rc, j0, o);
     pos += n;
   }
   return o;
 }
 
+// Wave-wide inclusive prefix sum.
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v, int lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  return v;
+}
+
+struct TileDesc {
+  uint64_t T0, T1, Q0, Q1;
+  uint32_t eb, m, tb, nt;
+};
+
+__device__ __forceinline__ TileDesc load_desc(const ExtractArgs& a, uint32_t t) {
+  TileDesc d;
+  d.T0 = a.tile_start[t];
+  d.T1 = a.tile_start[t + 1];
+  d.Q0 = a.tile_q[t];
+  d.Q1 = a.tile_q[t + 1];
+  d.eb = a.tile_ex[2 * t];
+  d.m = a.tile_ex[2 * t + 1] - d.eb;
+  d.tb = a.tile_tx[2 * t];
+  d.nt = a.tile_tx[2 * t + 1] - d.tb;
+  return d;
+}
+
+// Per-lane rows of one tile: intervals lane and lane+64, record lane.
+struct TileRows {
+  uint64_t o0[2], o1[2], g[2];
+  uint64_t tn, tp, tq;
+};
+
+__device__ __forceinline__ TileRows load_rows(const ExtractArgs& a, const TileDesc& d, int lane) {
+  TileRows r;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t j = min((uint32_t)(lane + 64 * h), d.m);  // clamped: rows stay in bounds
+    r.o0[h] = a.ex_out[d.eb + j];
+    r.o1[h] = a.ex_out[d.eb + j + 1];
+    r.g[h] = a.ex_g[d.eb + j];
+  }
+  const uint32_t j = min((uint32_t)lane, d.nt);
+  r.tn = a.tx_nuc[d.tb + j];
+  r.tp = a.tx_pep[d.tb + j];
+  r.tq = a.tx_pep[d.tb + j + 1];
+  return r;
+}
+
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
-  __shared__ uint64_t s_anchor[kExonCap];
-  __shared__ int32_t s_es[kExonCap + 1];
-  __shared__ uint8_t s_rc[kExonCap];
-  __shared__ uint16_t s_cmap[kLdsChunks];
-  __shared__ uint32_t s_codes[kLdsChunks];
-  __shared__ uint32_t s_valid32[kLdsChunks / 2 + 2];
-  __shared__ int64_t s_tn[kTxCap + 1];
-  __shared__ int64_t s_tp[kTxCap + 1];
-  __shared__ uint16_t s_pmap[kPepChunks + 2];
+  __shared__ WaveLds s_wave[kWaves];
   __shared__ uint32_t s_lut[64];
 
-  uint16_t* s_valid = reinterpret_cast<uint16_t*>(s_valid32);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  WaveLds& L = s_wave[wave];
+  uint32_t* const codes = L.codes_g + kGuard;
+  uint32_t* const valid32 = L.valid_g + kGuard;
+  uint16_t* const valid16 = reinterpret_cast<uint16_t*>(valid32);
   const Planes pl{a.codes, a.lower, a.dir, a.runs};
-  const int tid = threadIdx.x;
-  const uint32_t tile = blockIdx.x;
-  const uint64_t T0 = a.tile_start[tile];
-  const uint64_t T1 = a.tile_start[tile + 1];
-  const uint32_t eb = a.tile_ex[2 * tile];
-  const int m = (int)(a.tile_ex[2 * tile + 1] - eb);
-  const uint32_t tb = a.tile_tx[2 * tile];
-  const int nt = (int)(a.tile_tx[2 * tile + 1] - tb);
-  const uint64_t Q0 = a.tile_q[tile];
-  const uint64_t Q1 = a.tile_q[tile + 1];
-
-  const int span = (int)(T1 - T0);                                       // bytes stored
-  const int lim = (int)min((uint64_t)(span + kHalo), a.total_nuc - T0);  // bytes decoded
-  const int n_out = (span + kChunk - 1) / kChunk;
-  const int n_all = (lim + kChunk - 1) / kChunk;
-  const uint64_t qbase = Q0 & ~15ull;
-  const int qshift = (int)(Q0 - qbase);
-  const int n_res = (int)(Q1 - Q0);
-  const int n_pc = (n_res + qshift + 15) >> 4;
-
-  // ---- prologue: stage intervals / records, scatter chunk owners -----------
-  if (tid < 64) s_lut[tid] = (a.lut[tid >> 2] >> (8 * (tid & 3))) & 0xFFu;
-  for (int j = tid; j < m; j += kThreads) {
-    const uint64_t o0 = a.ex_out[eb + j];
-    const uint64_t o1 = a.ex_out[eb + j + 1];
-    const uint64_t gw = a.ex_g[eb + j];
-    const bool rc = (gw & kRcBit) != 0;
-    const uint64_t g = gw & ~kRcBit;
-    const int64_t s = (int64_t)(o0 - T0);
-    const int64_t e = (int64_t)(o1 - T0);
-    s_anchor[j] = rc ? g + (o1 - o0) - 1 + (uint64_t)s : g - (uint64_t)s;
-    s_rc[j] = rc ? 1 : 0;
-    const int s32 = s < 0 ? 0 : (int)s;
-    const int e32 = e > (int64_t)(kTile + 2 * kHalo) ? kTile + 2 * kHalo : (int)e;
-    s_es[j] = s32;
-    if (j == m - 1) s_es[m] = e32;
-    const int c_hi = min((e32 + kChunk - 1) / kChunk, n_all);
-    for (int c = (s32 + kChunk - 1) / kChunk; c < c_hi; ++c) s_cmap[c] = (uint16_t)j;
-  }
-  for (int j = tid; j < nt; j += kThreads) {
-    const int64_t tn = (int64_t)(a.tx_nuc[tb + j] - T0);
-    const int64_t tp = (int64_t)(a.tx_pep[tb + j] - Q0);
-    const int64_t tq = (int64_t)(a.tx_pep[tb + j + 1] - Q0);
-    s_tn[j] = tn;
-    s_tp[j] = tp;
-    if (j == nt - 1) s_tp[nt] = tq;
-    // residue chunk c starts at relative residue max(16c - qshift, 0)
-    const int64_t lo = tp <= 0 ? 0 : (tp + qshift + 15) / 16;
-    const int64_t hi = min((tq + qshift + 15) / 16, (int64_t)n_pc);
-    for (int64_t c = lo; c < hi; ++c) s_pmap[c] = (uint16_t)j;
-  }
-  __syncthreads();
-
-  // ---- nucleotide phase: up to 3 chunks per lane + 1 halo chunk -----------
   const bool want_nuc = (a.outputs & MAGOT_OUT_NUC) != 0;
-  uint32_t t[kChunksPerThread], lt[kChunksPerThread], d0[kChunksPerThread],
-      d1[kChunksPerThread];
-  bool single[kChunksPerThread];
-  int ex_i[kChunksPerThread];
-#pragma unroll
-  for (int k = 0; k < kChunksPerThread; ++k) {
-    const int c = tid + k * kThreads;
-    const int p = c * kChunk;
-    single[k] = false;
-    ex_i[k] = 0;
-    if (c < n_all) {
-      const int i = s_cmap[c];
-      ex_i[k] = i;
-      single[k] = s_es[i + 1] >= min(p + kChunk, lim);
-    }
-    if (single[k]) {
-      const int i = ex_i[k];
-      const uint64_t A = s_anchor[i];
-      const bool rc = s_rc[i] != 0;
-      const int n = min(p + kChunk, lim) - p;
-      const uint64_t glo = rc ? A - (uint64_t)(p + n - 1) : A + (uint64_t)p;
-      const uint64_t ghi = glo + (uint64_t)(n - 1);
-      window(pl, rc ? A - (uint64_t)p - 15 : glo, t[k], lt[k]);
-      d0[k] = a.dir[glo >> kDirShift];
-      d1[k] = a.dir[ghi >> kDirShift];
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kChunksPerThread + 1; ++k) {
-    const int c = tid + k * kThreads;
-    if (k == kChunksPerThread && tid != 0) break;
-    if (c >= n_all) continue;
-    const int p = c * kChunk;
-    Chunk o;
-    if (k < kChunksPerThread && single[k]) {
-      const int i = ex_i[k];
-      const bool rc = s_rc[i] != 0;
-      const int n = min(p + kChunk, lim) - p;
-      uint32_t tt = t[k], ll = lt[k];
-      if (rc) {
-        tt = ~rev_pairs(tt);
-        ll = __builtin_bitreverse32(ll) >> 16;
-      }
-      const uint32_t m1 = n >= 16 ? 0xFFFFu : ((1u << n) - 1u);
-      o.codes = n >= 16 ? tt : (tt & ((1u << (2 * n)) - 1u));
-      o.low = ll & m1;
-      o.exc = 0;
-      o.lit[0] = o.lit[1] = o.lit[2] = o.lit[3] = 0;
-      if (!((d0[k] & kDirClean) && (d1[k] & kDirClean))) {
-        const uint64_t A = s_anchor[i];
-        const uint64_t glo = rc ? A - (uint64_t)(p + n - 1) : A + (uint64_t)p;
-        o = patch_runs(a.runs, d0[k] & ~kDirClean, glo, glo + (uint64_t)(n - 1), rc, 0, o);
-      }
-    } else {
-      o = build_chunk_slow(pl, p, lim, s_cmap[c], s_es, s_anchor, s_rc);
-    }
-    if (want_nuc && c < n_out) *reinterpret_cast<uint4*>(a.nuc + T0 + p) = chunk_ascii(o);
-    s_codes[c] = o.codes;
-    s_valid[c] = (uint16_t)(~o.exc);
-  }
-  if (!(a.outputs & MAGOT_OUT_PEP) || n_res <= 0) return;
-  if (tid < 4) {
-    // zero the tail so window reads past the decoded bytes see defined words
-    s_codes[n_all + tid] = 0;
-    s_valid[n_all + tid] = 0;
-  }
-  __syncthreads();
+  const bool want_pep = (a.outputs & MAGOT_OUT_PEP) != 0;
 
-  // ---- translation phase ---------------------------------------------------
-  for (int c = tid; c < n_pc; c += kThreads) {
-    const int kk0 = c == 0 ? qshift : 0;                   // first residue slot used
-    const int q_first = c * 16 - qshift;                   // residue of slot 0 (rel Q0)
-    const int kk1 = min(16, n_res - q_first);              // slots [kk0, kk1)
-    int j = s_pmap[c];
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (kk0 == 0 && kk1 == 16 && (int64_t)(q_first + 16) <= s_tp[j + 1]) {
-      // 16 residues of one record: codons at r0, r0+3, ..., r0+45
-      const int r0 = (int)(s_tn[j] + 3 * ((int64_t)q_first - s_tp[j]));
-      const int cw = r0 >> 4;
-      const uint32_t sh = (uint32_t)(2 * (r0 & 15));
-      const uint32_t X0 = s_codes[cw], X1 = s_codes[cw + 1], X2 = s_codes[cw + 2],
-                     X3 = s_codes[cw + 3], X4 = s_codes[cw + 4];
-      const uint32_t Y[4] = {funnel(X1, X0, sh), funnel(X2, X1, sh), funnel(X3, X2, sh),
-                             funnel(X4, X3, sh)};
-      const int vw = r0 >> 5;
-      const uint32_t vsh = (uint32_t)(r0 & 31);
-      const uint32_t V0 = s_valid32[vw], V1 = s_valid32[vw + 1], V2 = s_valid32[vw + 2];
-      const uint32_t Z0 = funnel(V1, V0, vsh), Z1 = funnel(V2, V1, vsh);
-      // bit 3k of OK = all three bases of codon k are plain ACGT
-      const uint32_t ok0 = Z0 & funnel(Z1, Z0, 1) & funnel(Z1, Z0, 2);
-      const uint32_t ok1 = Z1 & (Z1 >> 1) & (Z1 >> 2);
+  if (threadIdx.x < 64)
+    s_lut[threadIdx.x] = (a.lut[threadIdx.x >> 2] >> (8 * (threadIdx.x & 3))) & 0xFFu;
+  if (lane < kGuard) {
+    L.codes_g[lane] = 0;
+    L.valid_g[lane] = 0;
+  }
+  __syncthreads();  // the only block-level barrier: s_lut
+
+  const uint32_t stride = gridDim.x * kWaves;
+  uint32_t t = blockIdx.x * kWaves + wave;
+  if (t >= a.n_tiles) return;
+  TileDesc d = load_desc(a, t);
+  TileRows rows = load_rows(a, d, lane);
+
+  for (; t < a.n_tiles; t += stride) {
+    const uint64_t T0 = d.T0, Q0 = d.Q0;
+    const int span = (int)(d.T1 - T0);
+    const int lim = (int)min((uint64_t)(span + kHalo), a.total_nuc - T0);
+    const int n_out = (span + kChunk - 1) / kChunk;
+    const int n_all = (lim + kChunk - 1) / kChunk;
+    const uint64_t qbase = Q0 & ~15ull;
+    const int qshift = (int)(Q0 - qbase);
+    const int n_res = (int)(d.Q1 - Q0);
+    const int n_pc = (n_res + qshift + 15) >> 4;
+    const int m = (int)d.m, nt = (int)d.nt;
+
+    // ---- staging: interval / record rows -> LDS, histograms -> maps ------
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int ob = 6 * k;
-        const uint32_t idx = ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
-                                              : funnel(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
-                             63u;
-        const int vb = 3 * k;
-        const uint32_t okb = vb < 32 ? (ok0 >> vb) : (ok1 >> (vb - 32));
-        const uint32_t aa = (okb & 1u) ? s_lut[idx] : (uint32_t)'X';
-        w[k >> 2] |= aa << (8 * (k & 3));
-      }
-      *reinterpret_cast<uint4*>(a.pep + qbase + 16 * (uint64_t)c) = make_uint4(w[0], w[1], w[2], w[3]);
-    } else {
-      for (int kk = kk0; kk < kk1; ++kk) {
-        const int q = q_first + kk;
-        while ((int64_t)q >= s_tp[j + 1]) ++j;
-        const int r = (int)(s_tn[j] + 3 * ((int64_t)q - s_tp[j]));
-        const int cw = r >> 4;
-        const uint32_t x = funnel(s_codes[cw + 1], s_codes[cw], (uint32_t)(2 * (r & 15))) & 63u;
-        const uint32_t v = funnel(s_valid32[(r >> 5) + 1], s_valid32[r >> 5], (uint32_t)(r & 31));
-        const uint32_t aa = ((v & 7u) == 7u) ? s_lut[x] : (uint32_t)'X';
-        a.pep[qbase + 16 * (uint64_t)c + kk] = (uint8_t)aa;
+    for (int h = 0; h < 3; ++h) codes[lane + 64 * h] = 0;
+    valid32[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = lane + 64 * h;
+      if (j < m) {
+        const uint64_t o0 = rows.o0[h], o1 = rows.o1[h], gw = rows.g[h];
+        const bool rc = (gw & kRcBit) != 0;
+        const uint64_t g = gw & ~(kRcBit | kExcBit);
+        const int64_t s = (int64_t)(o0 - T0);
+        const int64_t e = (int64_t)(o1 - T0);
+        const uint64_t A = rc ? g + (o1 - o0) - 1 + (uint64_t)s : g - (uint64_t)s;
+        const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
+        const uint32_t fl = (rc ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u);
+        L.ex[j] = make_uint4((uint32_t)A, (uint32_t)(A >> 32), end32, fl);
+        if (j >= 1) {
+          const int cj = ((int)s + kChunk - 1) / kChunk;
+          if (cj < n_all) atomicAdd(&codes[cj], 1u);
+        }
       }
     }
+    if (lane < nt) {
+      const int64_t tn = (int64_t)(rows.tn - T0);
+      const int64_t tp = (int64_t)(rows.tp - Q0);
+      L.tn[lane] = tn;
+      L.tp[lane] = tp;
+      if (lane == nt - 1) L.tp[nt] = (int64_t)(rows.tq - Q0);
+      if (lane >= 1) {
+        const int pj = ((int)tp + qshift + 15) >> 4;
+        if (pj < n_pc) atomicAdd(&valid32[pj], 1u);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    {
+      const uint32_t h0 = codes[3 * lane], h1 = codes[3 * lane + 1], h2 = codes[3 * lane + 2];
+      const uint32_t p0 = valid32[lane];
+      const uint32_t c0 = h0, c1 = h0 + h1, c2 = h0 + h1 + h2;
+      const uint32_t cx = wave_scan(c2, lane) - c2;
+      const uint32_t px = wave_scan(p0, lane);
+      L.cmap[3 * lane] = (uint8_t)(cx + c0);
+      L.cmap[3 * lane + 1] = (uint8_t)(cx + c1);
+      L.cmap[3 * lane + 2] = (uint8_t)(cx + c2);
+      L.pmap[lane] = (uint8_t)px;
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- nucleotide phase: issue every window load, then prefetch --------
+    uint2 cA[kLaneChunks], lA[kLaneChunks], cB[kLaneChunks], lB[kLaneChunks];
+    uint32_t shA[kLaneChunks], shB[kLaneChunks], n1s[kLaneChunks], info[kLaneChunks];
+#pragma unroll
+    for (int k = 0; k < kLaneChunks; ++k) {
+      const int c = lane + 64 * k;
+      const int p = c * kChunk;
+      info[k] = 0;  // bit0 active, bit1 rcA, bit2 two segs, bit3 rcB, bit4 slow
+      if (c < n_all) {
+        const int i = L.cmap[c];
+        const uint4 X = L.ex[i];
+        const int cend = min(p + kChunk, lim);
+        const uint64_t A = (uint64_t)X.x | ((uint64_t)X.y << 32);
+        const bool rcA = (X.w & kFlagRc) != 0;
+        const uint64_t wa = rcA ? A - (uint64_t)p - 15 : A + (uint64_t)p;
+        uint32_t inf = 1u | (rcA ? 2u : 0u);
+        bool slow = (X.w & kFlagExc) != 0;
+        const int n1 = (int)X.z - p;
+        n1s[k] = (uint32_t)n1;
+        shA[k] = (uint32_t)wa;
+        if (!(a.outputs & kDebugNoLoads)) {
+          cA[k] = *reinterpret_cast<const uint2*>(a.codes + (wa >> 4));
+          lA[k] = *reinterpret_cast<const uint2*>(a.lower + (wa >> 5));
+        } else {
+          cA[k] = make_uint2((uint32_t)wa, 0u);
+          lA[k] = make_uint2(0u, 0u);
+        }
+        if (n1 < cend - p) {
+          const uint4 Y = L.ex[i + 1];
+          const uint64_t B2 = (uint64_t)Y.x | ((uint64_t)Y.y << 32);
+          const bool rcB = (Y.w & kFlagRc) != 0;
+          const uint64_t wb = rcB ? B2 - (uint64_t)p - 15 : B2 + (uint64_t)p;
+          inf |= 4u | (rcB ? 8u : 0u);
+          slow = slow || (Y.w & kFlagExc) != 0 || (int)Y.z < cend;
+          shB[k] = (uint32_t)wb;
+          cB[k] = *reinterpret_cast<const uint2*>(a.codes + (wb >> 4));
+          lB[k] = *reinterpret_cast<const uint2*>(a.lower + (wb >> 5));
+        }
+        if (slow || (a.outputs & kDebugSlowNuc)) inf |= 16u;
+        info[k] = inf;
+      }
+    }
+
+    // prefetch the next tile while this one computes
+    const uint32_t t_next = t + stride;
+    TileDesc dn = d;
+    TileRows rn = rows;
+    if (t_next < a.n_tiles) {
+      dn = load_desc(a, t_next);
+      rn = load_rows(a, dn, lane);
+    }
+
+#pragma unroll
+    for (int k = 0; k < kLaneChunks; ++k) {
+      const int c = lane + 64 * k;
+      const int p = c * kChunk;
+      const uint32_t inf = info[k];
+      if (!(inf & 1u)) continue;
+      uint32_t cw, lw, ex = 0;
+      uint32_t lit[4] = {0u, 0u, 0u, 0u};
+      if (!(inf & 16u)) {
+        uint32_t t1 = funnel(cA[k].y, cA[k].x, 2 * (shA[k] & 15));
+        uint32_t l1 = funnel(lA[k].y, lA[k].x, shA[k] & 31) & 0xFFFFu;
+        if (inf & 2u) {
+          t1 = ~rev_pairs(t1);
+          l1 = __builtin_bitreverse32(l1) >> 16;
+        }
+        cw = t1;
+        lw = l1;
+        if (inf & 4u) {
+          uint32_t t2 = funnel(cB[k].y, cB[k].x, 2 * (shB[k] & 15));
+          uint32_t l2 = funnel(lB[k].y, lB[k].x, shB[k] & 31) & 0xFFFFu;
+          if (inf & 8u) {
+            t2 = ~rev_pairs(t2);
+            l2 = __builtin_bitreverse32(l2) >> 16;
+          }
+          const uint32_t n1 = n1s[k];  // 1..15
+          const uint32_t m2 = (1u << (2 * n1)) - 1u;
+          const uint32_t m1 = (1u << n1) - 1u;
+          cw = (t1 & m2) | (t2 & ~m2);
+          lw = (l1 & m1) | (l2 & ~m1);
+        }
+      } else {
+        const Chunk o = build_chunk_slow(pl, p, lim, L.cmap[c], L.ex);
+        cw = o.codes;
+        lw = o.low;
+        ex = o.exc;
+        lit[0] = o.lit[0];
+        lit[1] = o.lit[1];
+        lit[2] = o.lit[2];
+        lit[3] = o.lit[3];
+      }
+      if (want_nuc && c < n_out)
+        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) = chunk_ascii(cw, lw, ex, lit);
+      codes[c] = cw;
+      valid16[c] = (uint16_t)~ex;
+    }
+
+    if (want_pep && n_res > 0 && !(a.outputs & kDebugPrologueOnly)) {
+      if (lane < 5) {
+        codes[n_all + lane] = 0;  // defined words past the decoded bytes
+        valid16[n_all + lane] = 0;
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- translation phase: one residue chunk per lane -------------------
+      {
+        const int c = lane;
+        const int q_first = c * 16 - qshift;               // residue of slot 0 (rel Q0)
+        const int kk0 = c == 0 ? qshift : 0;
+        const int kk1 = min(16, n_res - q_first);
+        const int j = c < n_pc ? L.pmap[c] : 0;
+        const int64_t tpj = L.tp[j], tpn = L.tp[j + 1];
+        // segment 1: record j from slot 0; segment 2: record j+1 from slot s
+        const int r1 = (int)(L.tn[j] + 3 * ((int64_t)q_first - tpj));
+        const int s = (int)min(tpn - (int64_t)q_first, (int64_t)16);
+        const bool two = s < kk1;
+        int r2 = 0;
+        bool slow = (a.outputs & kDebugSlowPep) != 0;
+        if (two) {
+          r2 = (int)L.tn[j + 1] - 3 * s;                   // >= r1 (record j+1 follows j)
+          slow = slow || (L.tp[j + 2] - (int64_t)q_first) < (int64_t)kk1;
+        }
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        if (c >= n_pc) {
+          // no residue chunk for this lane
+        } else if (!slow) {
+#pragma unroll 1
+          for (int seg = 0; seg < 2; ++seg) {
+            if (seg == 1 && !two) break;
+            const int r0 = seg == 0 ? r1 : r2;
+            const int cw = r0 >> 4;
+            const uint32_t sh = (uint32_t)(2 * (r0 & 15));
+            const uint32_t X0 = codes[cw], X1 = codes[cw + 1], X2 = codes[cw + 2],
+                           X3 = codes[cw + 3], X4 = codes[cw + 4];
+            const uint32_t Y[4] = {funnel(X1, X0, sh), funnel(X2, X1, sh), funnel(X3, X2, sh),
+                                   funnel(X4, X3, sh)};
+            const int vw = r0 >> 5;
+            const uint32_t vsh = (uint32_t)(r0 & 31);
+            const uint32_t V0 = valid32[vw], V1 = valid32[vw + 1], V2 = valid32[vw + 2];
+            const uint32_t Z0 = funnel(V1, V0, vsh), Z1 = funnel(V2, V1, vsh);
+            // bit 3k of ok = all three bases of codon k are plain ACGT
+            const uint32_t ok0 = Z0 & funnel(Z1, Z0, 1) & funnel(Z1, Z0, 2);
+            const uint32_t ok1 = Z1 & (Z1 >> 1) & (Z1 >> 2);
+            uint32_t v[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+              const int ob = 6 * k;
+              const uint32_t idx =
+                  ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
+                                   : funnel(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
+                  63u;
+              const int vb = 3 * k;
+              const uint32_t okb = vb < 32 ? (ok0 >> vb) : (ok1 >> (vb - 32));
+              const uint32_t aa = (okb & 1u) ? s_lut[idx] : (uint32_t)'X';
+              v[k >> 2] |= aa << (8 * (k & 3));
+            }
+            if (seg == 0) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) w[q] = v[q];
+            } else {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const int nb = min(max(s - 4 * q, 0), 4);  // bytes of word q from segment 1
+                const uint32_t keep = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+                w[q] = (w[q] & keep) | (v[q] & ~keep);
+              }
+            }
+          }
+        } else {
+          int jj = j;
+          for (int kk = kk0; kk < kk1; ++kk) {
+            const int q = q_first + kk;
+            while ((int64_t)q >= L.tp[jj + 1]) ++jj;
+            const int r = (int)(L.tn[jj] + 3 * ((int64_t)q - L.tp[jj]));
+            const int cw = r >> 4;
+            const uint32_t x = funnel(codes[cw + 1], codes[cw], (uint32_t)(2 * (r & 15))) & 63u;
+            const uint32_t vv =
+                funnel(valid32[(r >> 5) + 1], valid32[r >> 5], (uint32_t)(r & 31));
+            const uint32_t aa = ((vv & 7u) == 7u) ? s_lut[x] : (uint32_t)'X';
+            w[kk >> 2] |= aa << (8 * (kk & 3));
+          }
+        }
+        uint8_t* dst = a.pep + qbase + 16 * (uint64_t)c;
+        if (c >= n_pc) {
+        } else if (kk0 == 0 && kk1 == 16) {
+          *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < 16; ++kk)
+            if (kk >= kk0 && kk < kk1) dst[kk] = (uint8_t)(w[kk >> 2] >> (8 * (kk & 3)));
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    d = dn;
+    rows = rn;
   }
 }
 
@@ -373,7 +539,16 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
 
 void launch_extract(const ExtractArgs& a, hipStream_t s) {
   if (a.n_tiles == 0) return;
-  hipLaunchKernelGGL(extract_kernel, dim3(a.n_tiles), dim3(kThreads), 0, s, a);
+  const uint32_t need = (a.n_tiles + kWaves - 1) / kWaves;
+  const uint32_t grid = min(need, a.grid ? a.grid : need);
+  hipLaunchKernelGGL(extract_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+}
+
+int extract_blocks_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extract_kernel, kThreads, 0) != hipSuccess)
+    return 0;
+  return n;
 }
 
 }  // namespace magot

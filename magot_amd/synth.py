@@ -213,8 +213,34 @@ def _transcripts(rng, contig_len, n_tx, mean_extra_exons=7, ex_lo=50, ex_hi=250,
         ex_start.astype(np.int64), ex_len.astype(np.int64)
 
 
-def make(config, seed=None, genome_bases=None, n_tx=None, iupac_rate=None):
-    """Build a named workload.  ``genome_bases`` / ``n_tx`` rescale it (tests)."""
+def _sort_by_position(w):
+    """Order transcripts by (contig, start) as a coordinate-sorted GFF lists them."""
+    first = np.concatenate([[0], np.cumsum(w.ex_count)])
+    key = w.tx_contig * (1 << 40) + w.ex_start[first[:-1]]
+    order = np.argsort(key, kind='stable')
+    idx = np.concatenate([np.arange(first[t], first[t + 1]) for t in order]) if len(order) \
+        else np.zeros(0, np.int64)
+    w.tx_contig = w.tx_contig[order]
+    w.tx_strand = w.tx_strand[order]
+    w.ex_count = w.ex_count[order]
+    w.ex_start = w.ex_start[idx]
+    w.ex_len = w.ex_len[idx]
+    return w
+
+
+def make(config, seed=None, genome_bases=None, n_tx=None, iupac_rate=None, order='random'):
+    """Build a named workload.  ``genome_bases`` / ``n_tx`` rescale it (tests).
+    ``order``: 'random' (transcripts in placement order within each contig) or
+    'sorted' (by start coordinate, as a coordinate-sorted GFF)."""
+    w = _make(config, seed, genome_bases, n_tx, iupac_rate)
+    if order == 'sorted':
+        w = _sort_by_position(w)
+    elif order != 'random':
+        raise ValueError(order)
+    return w
+
+
+def _make(config, seed, genome_bases, n_tx, iupac_rate):
     idx = {'C2': 2, 'C3': 3, 'C5': 5, 'small': 9}[config]
     rng = np.random.default_rng(SEED_BASE + idx if seed is None else seed)
     if config == 'C2':

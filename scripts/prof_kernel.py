@@ -12,11 +12,14 @@ from magot_amd import _lib, engine, synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument('--config', default='C3')
 ap.add_argument('--iters', type=int, default=10)
+ap.add_argument('--order', default='random')
+ap.add_argument('--outputs', default='nuc+pep')
 a = ap.parse_args()
-w = synth.make(a.config)
+w = synth.make(a.config, order=a.order)
 dev = engine.DeviceGenome(w.contigs())
 ex, tx = w.plan_tables()
-outputs = engine.OUT_NUC | (engine.OUT_PEP if w.outputs == 'nuc+pep' else 0)
+outputs = {'nuc+pep': engine.OUT_NUC | engine.OUT_PEP, 'nuc': engine.OUT_NUC,
+           'pep': engine.OUT_PEP}[a.outputs]
 plan = engine.ExtractionPlan(dev, ex, tx, outputs)
 for _ in range(a.iters):
     plan.execute()
