@@ -212,16 +212,24 @@ struct TileDesc {
   uint32_t eb, m, tb, nt;
 };
 
+// Uniform loads through the constant address space: scalar (s_load) even in
+// the persistent loop after vector stores.
+template <class T>
+__device__ __forceinline__ T sload(const T* p, uint32_t i) {
+  typedef const __attribute__((address_space(4))) T CT;
+  return ((CT*)p)[i];
+}
+
 __device__ __forceinline__ TileDesc load_desc(const ExtractArgs& a, uint32_t t) {
   TileDesc d;
-  d.T0 = a.tile_start[t];
-  d.T1 = a.tile_start[t + 1];
-  d.Q0 = a.tile_q[t];
-  d.Q1 = a.tile_q[t + 1];
-  d.eb = a.tile_ex[2 * t];
-  d.m = a.tile_ex[2 * t + 1] - d.eb;
-  d.tb = a.tile_tx[2 * t];
-  d.nt = a.tile_tx[2 * t + 1] - d.tb;
+  d.T0 = sload(a.tile_start, t);
+  d.T1 = sload(a.tile_start, t + 1);
+  d.Q0 = sload(a.tile_q, t);
+  d.Q1 = sload(a.tile_q, t + 1);
+  d.eb = sload(a.tile_ex, 2 * t);
+  d.m = sload(a.tile_ex, 2 * t + 1) - d.eb;
+  d.tb = sload(a.tile_tx, 2 * t);
+  d.nt = sload(a.tile_tx, 2 * t + 1) - d.tb;
   return d;
 }
 
@@ -247,6 +255,102 @@ __device__ __forceinline__ TileRows load_rows(const ExtractArgs& a, const TileDe
   return r;
 }
 
+// Derived per-tile quantities (all wave-uniform).
+struct TileGeom {
+  int span, lim, n_out, n_all, qshift, n_res, n_pc;
+  uint64_t qbase;
+};
+
+__device__ __forceinline__ TileGeom geom(const ExtractArgs& a, const TileDesc& d) {
+  TileGeom g;
+  g.span = (int)(d.T1 - d.T0);
+  g.lim = (int)min((uint64_t)(g.span + kHalo), a.total_nuc - d.T0);
+  g.n_out = (g.span + kChunk - 1) / kChunk;
+  g.n_all = (g.lim + kChunk - 1) / kChunk;
+  g.qbase = d.Q0 & ~15ull;
+  g.qshift = (int)(d.Q0 - g.qbase);
+  g.n_res = (int)(d.Q1 - d.Q0);
+  g.n_pc = (g.n_res + g.qshift + 15) >> 4;
+  return g;
+}
+
+// Stage one tile into the wave's LDS: interval rows {anchor, end, flags},
+// record rows, and the chunk->interval / residue chunk->record maps
+// (histogram of first chunks + wave prefix scan).
+__device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* valid32,
+                                      const TileDesc& d, const TileGeom& g, const TileRows& rows,
+                                      int lane) {
+  const int m = (int)d.m, nt = (int)d.nt;
+#pragma unroll
+  for (int h = 0; h < 3; ++h) codes[lane + 64 * h] = 0;
+  valid32[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = lane + 64 * h;
+    if (j < m) {
+      const uint64_t o0 = rows.o0[h], o1 = rows.o1[h], gw = rows.g[h];
+      const bool rc = (gw & kRcBit) != 0;
+      const uint64_t gs = gw & ~(kRcBit | kExcBit);
+      const int64_t s = (int64_t)(o0 - d.T0);
+      const int64_t e = (int64_t)(o1 - d.T0);
+      const uint64_t A = rc ? gs + (o1 - o0) - 1 + (uint64_t)s : gs - (uint64_t)s;
+      const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
+      const uint32_t fl = (rc ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u);
+      L.ex[j] = make_uint4((uint32_t)A, (uint32_t)(A >> 32), end32, fl);
+      if (j >= 1) {
+        const int cj = ((int)s + kChunk - 1) / kChunk;
+        if (cj < g.n_all) atomicAdd(&codes[cj], 1u);
+      }
+    }
+  }
+  if (lane < nt) {
+    const int64_t tp = (int64_t)(rows.tp - d.Q0);
+    L.tn[lane] = (int64_t)(rows.tn - d.T0);
+    L.tp[lane] = tp;
+    if (lane == nt - 1) L.tp[nt] = (int64_t)(rows.tq - d.Q0);
+    if (lane >= 1) {
+      const int pj = ((int)tp + g.qshift + 15) >> 4;
+      if (pj < g.n_pc) atomicAdd(&valid32[pj], 1u);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t h0 = codes[3 * lane], h1 = codes[3 * lane + 1], h2 = codes[3 * lane + 2];
+  const uint32_t p0 = valid32[lane];
+  const uint32_t c1 = h0 + h1, c2 = c1 + h2;
+  const uint32_t cx = wave_scan(c2, lane) - c2;
+  const uint32_t px = wave_scan(p0, lane);
+  L.cmap[3 * lane] = (uint8_t)(cx + h0);
+  L.cmap[3 * lane + 1] = (uint8_t)(cx + c1);
+  L.cmap[3 * lane + 2] = (uint8_t)(cx + c2);
+  L.pmap[lane] = (uint8_t)px;
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Fast-path chunk assembly from prefetched windows (branch-free in the
+// strand and segment count; see meta bits in extract_kernel).
+__device__ __forceinline__ void fast_chunk(uint2 cA, uint2 lA, uint2 cB, uint2 lB, uint32_t mt,
+                                           uint32_t& cw, uint32_t& lw) {
+  const uint32_t sa = (mt >> 8) & 31u;
+  uint32_t t1 = funnel(cA.y, cA.x, 2 * (sa & 15));
+  uint32_t l1 = funnel(lA.y, lA.x, sa) & 0xFFFFu;
+  const uint32_t t1r = ~rev_pairs(t1), l1r = __builtin_bitreverse32(l1) >> 16;
+  t1 = (mt & 2u) ? t1r : t1;
+  l1 = (mt & 2u) ? l1r : l1;
+  const uint32_t sb = (mt >> 16) & 31u;
+  uint32_t t2 = funnel(cB.y, cB.x, 2 * (sb & 15));
+  uint32_t l2 = funnel(lB.y, lB.x, sb) & 0xFFFFu;
+  const uint32_t t2r = ~rev_pairs(t2), l2r = __builtin_bitreverse32(l2) >> 16;
+  t2 = (mt & 8u) ? t2r : t2;
+  l2 = (mt & 8u) ? l2r : l2;
+  // n1 = bytes from segment A (16 when the chunk is one segment)
+  const uint32_t n1 = (mt >> 24) & 31u;
+  const uint32_t m2 = n1 >= 16 ? 0xFFFFFFFFu : ((1u << (2 * n1)) - 1u);
+  const uint32_t m1 = n1 >= 16 ? 0xFFFFu : ((1u << n1) - 1u);
+  cw = (t1 & m2) | (t2 & ~m2);
+  lw = (l1 & m1) | (l2 & ~m1);
+}
+
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   __shared__ WaveLds s_wave[kWaves];
   __shared__ uint32_t s_lut[64];
@@ -257,7 +361,6 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   uint32_t* const codes = L.codes_g + kGuard;
   uint32_t* const valid32 = L.valid_g + kGuard;
   uint16_t* const valid16 = reinterpret_cast<uint16_t*>(valid32);
-  const Planes pl{a.codes, a.lower, a.dir, a.runs};
   const bool want_nuc = (a.outputs & MAGOT_OUT_NUC) != 0;
   const bool want_pep = (a.outputs & MAGOT_OUT_PEP) != 0;
 
@@ -269,269 +372,161 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   }
   __syncthreads();  // the only block-level barrier: s_lut
 
-  const uint32_t stride = gridDim.x * kWaves;
-  uint32_t t = blockIdx.x * kWaves + wave;
+  const uint32_t t = blockIdx.x * kWaves + wave;
   if (t >= a.n_tiles) return;
-  TileDesc d = load_desc(a, t);
-  TileRows rows = load_rows(a, d, lane);
+  const TileDesc d = load_desc(a, t);
+  const TileGeom g = geom(a, d);
+  stage(L, codes, valid32, d, g, load_rows(a, d, lane), lane);
+  const uint64_t T0 = d.T0;
 
-  for (; t < a.n_tiles; t += stride) {
-    const uint64_t T0 = d.T0, Q0 = d.Q0;
-    const int span = (int)(d.T1 - T0);
-    const int lim = (int)min((uint64_t)(span + kHalo), a.total_nuc - T0);
-    const int n_out = (span + kChunk - 1) / kChunk;
-    const int n_all = (lim + kChunk - 1) / kChunk;
-    const uint64_t qbase = Q0 & ~15ull;
-    const int qshift = (int)(Q0 - qbase);
-    const int n_res = (int)(d.Q1 - Q0);
-    const int n_pc = (n_res + qshift + 15) >> 4;
-    const int m = (int)d.m, nt = (int)d.nt;
-
-    // ---- staging: interval / record rows -> LDS, histograms -> maps ------
+  // ---- nucleotide chunks: issue every window load first -------------------
+  uint2 cA[kLaneChunks], lA[kLaneChunks], cB[kLaneChunks], lB[kLaneChunks];
+  uint32_t meta[kLaneChunks];  // bit0 active, 1 rcA, 3 rcB, 4 slow, 8..12 shiftA,
+                               // 16..20 shiftB, 24..28 bytes from segment A
 #pragma unroll
-    for (int h = 0; h < 3; ++h) codes[lane + 64 * h] = 0;
-    valid32[lane] = 0;
-    __builtin_amdgcn_wave_barrier();
+  for (int k = 0; k < kLaneChunks; ++k) {
+    const int c = min(lane + 64 * k, g.n_all - 1);  // clamped: inactive lanes redo a chunk
+    const int p = c * kChunk;
+    const int i = L.cmap[c];
+    const uint4 X = L.ex[i];
+    const uint4 Y = L.ex[min(i + 1, (int)d.m - 1)];
+    const int cend = min(p + kChunk, g.lim);
+    const uint64_t A = (uint64_t)X.x | ((uint64_t)X.y << 32);
+    const uint64_t B2 = (uint64_t)Y.x | ((uint64_t)Y.y << 32);
+    const bool rcA = (X.w & kFlagRc) != 0, rcB = (Y.w & kFlagRc) != 0;
+    const int n1 = min((int)X.z, cend) - p;       // bytes of segment A (1..16)
+    const bool two = n1 < cend - p;
+    const uint64_t wa = rcA ? A - (uint64_t)p - 15 : A + (uint64_t)p;
+    const uint64_t wb = two ? (rcB ? B2 - (uint64_t)p - 15 : B2 + (uint64_t)p) : wa;
+    const bool slow = ((X.w | (two ? Y.w : 0u)) & kFlagExc) != 0 || (two && (int)Y.z < cend) ||
+                      (a.outputs & kDebugSlowNuc);
+    meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (rcA ? 2u : 0u) | (rcB ? 8u : 0u) |
+              (slow ? 16u : 0u) | ((uint32_t)(wa & 31) << 8) | ((uint32_t)(wb & 31) << 16) |
+              ((uint32_t)(two ? n1 : 16) << 24);
+    cA[k] = *reinterpret_cast<const uint2*>(a.codes + (wa >> 4));
+    lA[k] = *reinterpret_cast<const uint2*>(a.lower + (wa >> 5));
+    cB[k] = *reinterpret_cast<const uint2*>(a.codes + (wb >> 4));
+    lB[k] = *reinterpret_cast<const uint2*>(a.lower + (wb >> 5));
+  }
+  uint32_t cwk[kLaneChunks], lwk[kLaneChunks];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = lane + 64 * h;
-      if (j < m) {
-        const uint64_t o0 = rows.o0[h], o1 = rows.o1[h], gw = rows.g[h];
-        const bool rc = (gw & kRcBit) != 0;
-        const uint64_t g = gw & ~(kRcBit | kExcBit);
-        const int64_t s = (int64_t)(o0 - T0);
-        const int64_t e = (int64_t)(o1 - T0);
-        const uint64_t A = rc ? g + (o1 - o0) - 1 + (uint64_t)s : g - (uint64_t)s;
-        const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
-        const uint32_t fl = (rc ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u);
-        L.ex[j] = make_uint4((uint32_t)A, (uint32_t)(A >> 32), end32, fl);
-        if (j >= 1) {
-          const int cj = ((int)s + kChunk - 1) / kChunk;
-          if (cj < n_all) atomicAdd(&codes[cj], 1u);
-        }
-      }
-    }
-    if (lane < nt) {
-      const int64_t tn = (int64_t)(rows.tn - T0);
-      const int64_t tp = (int64_t)(rows.tp - Q0);
-      L.tn[lane] = tn;
-      L.tp[lane] = tp;
-      if (lane == nt - 1) L.tp[nt] = (int64_t)(rows.tq - Q0);
-      if (lane >= 1) {
-        const int pj = ((int)tp + qshift + 15) >> 4;
-        if (pj < n_pc) atomicAdd(&valid32[pj], 1u);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    {
-      const uint32_t h0 = codes[3 * lane], h1 = codes[3 * lane + 1], h2 = codes[3 * lane + 2];
-      const uint32_t p0 = valid32[lane];
-      const uint32_t c0 = h0, c1 = h0 + h1, c2 = h0 + h1 + h2;
-      const uint32_t cx = wave_scan(c2, lane) - c2;
-      const uint32_t px = wave_scan(p0, lane);
-      L.cmap[3 * lane] = (uint8_t)(cx + c0);
-      L.cmap[3 * lane + 1] = (uint8_t)(cx + c1);
-      L.cmap[3 * lane + 2] = (uint8_t)(cx + c2);
-      L.pmap[lane] = (uint8_t)px;
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    // ---- nucleotide phase: issue every window load, then prefetch --------
-    uint2 cA[kLaneChunks], lA[kLaneChunks], cB[kLaneChunks], lB[kLaneChunks];
-    uint32_t shA[kLaneChunks], shB[kLaneChunks], n1s[kLaneChunks], info[kLaneChunks];
+  for (int k = 0; k < kLaneChunks; ++k) fast_chunk(cA[k], lA[k], cB[k], lB[k], meta[k], cwk[k], lwk[k]);
+  uint32_t slow_any = 0;
 #pragma unroll
-    for (int k = 0; k < kLaneChunks; ++k) {
-      const int c = lane + 64 * k;
-      const int p = c * kChunk;
-      info[k] = 0;  // bit0 active, bit1 rcA, bit2 two segs, bit3 rcB, bit4 slow
-      if (c < n_all) {
-        const int i = L.cmap[c];
-        const uint4 X = L.ex[i];
-        const int cend = min(p + kChunk, lim);
-        const uint64_t A = (uint64_t)X.x | ((uint64_t)X.y << 32);
-        const bool rcA = (X.w & kFlagRc) != 0;
-        const uint64_t wa = rcA ? A - (uint64_t)p - 15 : A + (uint64_t)p;
-        uint32_t inf = 1u | (rcA ? 2u : 0u);
-        bool slow = (X.w & kFlagExc) != 0;
-        const int n1 = (int)X.z - p;
-        n1s[k] = (uint32_t)n1;
-        shA[k] = (uint32_t)wa;
-        if (!(a.outputs & kDebugNoLoads)) {
-          cA[k] = *reinterpret_cast<const uint2*>(a.codes + (wa >> 4));
-          lA[k] = *reinterpret_cast<const uint2*>(a.lower + (wa >> 5));
-        } else {
-          cA[k] = make_uint2((uint32_t)wa, 0u);
-          lA[k] = make_uint2(0u, 0u);
-        }
-        if (n1 < cend - p) {
-          const uint4 Y = L.ex[i + 1];
-          const uint64_t B2 = (uint64_t)Y.x | ((uint64_t)Y.y << 32);
-          const bool rcB = (Y.w & kFlagRc) != 0;
-          const uint64_t wb = rcB ? B2 - (uint64_t)p - 15 : B2 + (uint64_t)p;
-          inf |= 4u | (rcB ? 8u : 0u);
-          slow = slow || (Y.w & kFlagExc) != 0 || (int)Y.z < cend;
-          shB[k] = (uint32_t)wb;
-          cB[k] = *reinterpret_cast<const uint2*>(a.codes + (wb >> 4));
-          lB[k] = *reinterpret_cast<const uint2*>(a.lower + (wb >> 5));
-        }
-        if (slow || (a.outputs & kDebugSlowNuc)) inf |= 16u;
-        info[k] = inf;
-      }
-    }
-
-    // prefetch the next tile while this one computes
-    const uint32_t t_next = t + stride;
-    TileDesc dn = d;
-    TileRows rn = rows;
-    if (t_next < a.n_tiles) {
-      dn = load_desc(a, t_next);
-      rn = load_rows(a, dn, lane);
-    }
-
+  for (int k = 0; k < kLaneChunks; ++k) slow_any |= meta[k] & 16u;
 #pragma unroll
-    for (int k = 0; k < kLaneChunks; ++k) {
-      const int c = lane + 64 * k;
-      const int p = c * kChunk;
-      const uint32_t inf = info[k];
-      if (!(inf & 1u)) continue;
-      uint32_t cw, lw, ex = 0;
-      uint32_t lit[4] = {0u, 0u, 0u, 0u};
-      if (!(inf & 16u)) {
-        uint32_t t1 = funnel(cA[k].y, cA[k].x, 2 * (shA[k] & 15));
-        uint32_t l1 = funnel(lA[k].y, lA[k].x, shA[k] & 31) & 0xFFFFu;
-        if (inf & 2u) {
-          t1 = ~rev_pairs(t1);
-          l1 = __builtin_bitreverse32(l1) >> 16;
-        }
-        cw = t1;
-        lw = l1;
-        if (inf & 4u) {
-          uint32_t t2 = funnel(cB[k].y, cB[k].x, 2 * (shB[k] & 15));
-          uint32_t l2 = funnel(lB[k].y, lB[k].x, shB[k] & 31) & 0xFFFFu;
-          if (inf & 8u) {
-            t2 = ~rev_pairs(t2);
-            l2 = __builtin_bitreverse32(l2) >> 16;
-          }
-          const uint32_t n1 = n1s[k];  // 1..15
-          const uint32_t m2 = (1u << (2 * n1)) - 1u;
-          const uint32_t m1 = (1u << n1) - 1u;
-          cw = (t1 & m2) | (t2 & ~m2);
-          lw = (l1 & m1) | (l2 & ~m1);
-        }
-      } else {
-        const Chunk o = build_chunk_slow(pl, p, lim, L.cmap[c], L.ex);
-        cw = o.codes;
-        lw = o.low;
-        ex = o.exc;
-        lit[0] = o.lit[0];
-        lit[1] = o.lit[1];
-        lit[2] = o.lit[2];
-        lit[3] = o.lit[3];
-      }
-      if (want_nuc && c < n_out)
-        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) = chunk_ascii(cw, lw, ex, lit);
-      codes[c] = cw;
+  for (int k = 0; k < kLaneChunks; ++k) {
+    const int c = lane + 64 * k;
+    const int p = c * kChunk;
+    const uint32_t mt = meta[k];
+    uint32_t ex = 0;
+    uint32_t lit[4] = {0u, 0u, 0u, 0u};
+    if (__builtin_amdgcn_readfirstlane(__ballot(slow_any != 0) != 0) && (mt & 17u) == 17u) {
+      const Planes pl{a.codes, a.lower, a.dir, a.runs};
+      const Chunk o = build_chunk_slow(pl, p, g.lim, L.cmap[c], L.ex);
+      cwk[k] = o.codes;
+      lwk[k] = o.low;
+      ex = o.exc;
+      lit[0] = o.lit[0];
+      lit[1] = o.lit[1];
+      lit[2] = o.lit[2];
+      lit[3] = o.lit[3];
+    }
+    if (mt & 1u) {
+      if (want_nuc && c < g.n_out)
+        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) = chunk_ascii(cwk[k], lwk[k], ex, lit);
+      codes[c] = cwk[k];
       valid16[c] = (uint16_t)~ex;
     }
+  }
+  if (!want_pep || g.n_res <= 0) return;
+  if (lane < 5) {
+    codes[g.n_all + lane] = 0;  // defined words past the decoded bytes
+    valid16[g.n_all + lane] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
 
-    if (want_pep && n_res > 0 && !(a.outputs & kDebugPrologueOnly)) {
-      if (lane < 5) {
-        codes[n_all + lane] = 0;  // defined words past the decoded bytes
-        valid16[n_all + lane] = 0;
-      }
-      __builtin_amdgcn_wave_barrier();
-      // ---- translation phase: one residue chunk per lane -------------------
-      {
-        const int c = lane;
-        const int q_first = c * 16 - qshift;               // residue of slot 0 (rel Q0)
-        const int kk0 = c == 0 ? qshift : 0;
-        const int kk1 = min(16, n_res - q_first);
-        const int j = c < n_pc ? L.pmap[c] : 0;
-        const int64_t tpj = L.tp[j], tpn = L.tp[j + 1];
-        // segment 1: record j from slot 0; segment 2: record j+1 from slot s
-        const int r1 = (int)(L.tn[j] + 3 * ((int64_t)q_first - tpj));
-        const int s = (int)min(tpn - (int64_t)q_first, (int64_t)16);
-        const bool two = s < kk1;
-        int r2 = 0;
-        bool slow = (a.outputs & kDebugSlowPep) != 0;
-        if (two) {
-          r2 = (int)L.tn[j + 1] - 3 * s;                   // >= r1 (record j+1 follows j)
-          slow = slow || (L.tp[j + 2] - (int64_t)q_first) < (int64_t)kk1;
-        }
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        if (c >= n_pc) {
-          // no residue chunk for this lane
-        } else if (!slow) {
+  // ---- translation: one residue chunk per lane ----------------------------
+  const int c = lane;
+  if (c >= g.n_pc) return;
+  const int q_first = c * 16 - g.qshift;  // residue of slot 0 (rel Q0)
+  const int kk0 = c == 0 ? g.qshift : 0;
+  const int kk1 = min(16, g.n_res - q_first);
+  const int j = L.pmap[c];
+  const int64_t tpj = L.tp[j], tpn = L.tp[j + 1];
+  // segment 1: record j from slot 0; segment 2: record j+1 from slot s
+  const int r1 = (int)(L.tn[j] + 3 * ((int64_t)q_first - tpj));
+  const int s = (int)min(tpn - (int64_t)q_first, (int64_t)16);
+  const bool two = s < kk1;
+  int r2 = 0;
+  bool slow = (a.outputs & kDebugSlowPep) != 0;
+  if (two) {
+    r2 = (int)L.tn[j + 1] - 3 * s;  // >= r1: record j+1 follows record j
+    slow = slow || (L.tp[j + 2] - (int64_t)q_first) < (int64_t)kk1;
+  }
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  if (!slow) {
 #pragma unroll 1
-          for (int seg = 0; seg < 2; ++seg) {
-            if (seg == 1 && !two) break;
-            const int r0 = seg == 0 ? r1 : r2;
-            const int cw = r0 >> 4;
-            const uint32_t sh = (uint32_t)(2 * (r0 & 15));
-            const uint32_t X0 = codes[cw], X1 = codes[cw + 1], X2 = codes[cw + 2],
-                           X3 = codes[cw + 3], X4 = codes[cw + 4];
-            const uint32_t Y[4] = {funnel(X1, X0, sh), funnel(X2, X1, sh), funnel(X3, X2, sh),
-                                   funnel(X4, X3, sh)};
-            const int vw = r0 >> 5;
-            const uint32_t vsh = (uint32_t)(r0 & 31);
-            const uint32_t V0 = valid32[vw], V1 = valid32[vw + 1], V2 = valid32[vw + 2];
-            const uint32_t Z0 = funnel(V1, V0, vsh), Z1 = funnel(V2, V1, vsh);
-            // bit 3k of ok = all three bases of codon k are plain ACGT
-            const uint32_t ok0 = Z0 & funnel(Z1, Z0, 1) & funnel(Z1, Z0, 2);
-            const uint32_t ok1 = Z1 & (Z1 >> 1) & (Z1 >> 2);
-            uint32_t v[4] = {0u, 0u, 0u, 0u};
+    for (int seg = 0; seg < 2; ++seg) {
+      if (seg == 1 && !two) break;
+      const int r0 = seg == 0 ? r1 : r2;
+      const int cw = r0 >> 4;
+      const uint32_t sh = (uint32_t)(2 * (r0 & 15));
+      const uint32_t X0 = codes[cw], X1 = codes[cw + 1], X2 = codes[cw + 2], X3 = codes[cw + 3],
+                     X4 = codes[cw + 4];
+      const uint32_t Y[4] = {funnel(X1, X0, sh), funnel(X2, X1, sh), funnel(X3, X2, sh),
+                             funnel(X4, X3, sh)};
+      const int vw = r0 >> 5;
+      const uint32_t vsh = (uint32_t)(r0 & 31);
+      const uint32_t V0 = valid32[vw], V1 = valid32[vw + 1], V2 = valid32[vw + 2];
+      const uint32_t Z0 = funnel(V1, V0, vsh), Z1 = funnel(V2, V1, vsh);
+      // bit 3k of ok = all three bases of codon k are plain ACGT
+      const uint32_t ok0 = Z0 & funnel(Z1, Z0, 1) & funnel(Z1, Z0, 2);
+      const uint32_t ok1 = Z1 & (Z1 >> 1) & (Z1 >> 2);
+      uint32_t v[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-              const int ob = 6 * k;
-              const uint32_t idx =
-                  ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
-                                   : funnel(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
-                  63u;
-              const int vb = 3 * k;
-              const uint32_t okb = vb < 32 ? (ok0 >> vb) : (ok1 >> (vb - 32));
-              const uint32_t aa = (okb & 1u) ? s_lut[idx] : (uint32_t)'X';
-              v[k >> 2] |= aa << (8 * (k & 3));
-            }
-            if (seg == 0) {
+      for (int k = 0; k < 16; ++k) {
+        const int ob = 6 * k;
+        const uint32_t idx = ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
+                                              : funnel(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
+                             63u;
+        const int vb = 3 * k;
+        const uint32_t okb = vb < 32 ? (ok0 >> vb) : (ok1 >> (vb - 32));
+        const uint32_t aa = (okb & 1u) ? s_lut[idx] : (uint32_t)'X';
+        v[k >> 2] |= aa << (8 * (k & 3));
+      }
+      if (seg == 0) {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) w[q] = v[q];
-            } else {
+        for (int q = 0; q < 4; ++q) w[q] = v[q];
+      } else {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const int nb = min(max(s - 4 * q, 0), 4);  // bytes of word q from segment 1
-                const uint32_t keep = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-                w[q] = (w[q] & keep) | (v[q] & ~keep);
-              }
-            }
-          }
-        } else {
-          int jj = j;
-          for (int kk = kk0; kk < kk1; ++kk) {
-            const int q = q_first + kk;
-            while ((int64_t)q >= L.tp[jj + 1]) ++jj;
-            const int r = (int)(L.tn[jj] + 3 * ((int64_t)q - L.tp[jj]));
-            const int cw = r >> 4;
-            const uint32_t x = funnel(codes[cw + 1], codes[cw], (uint32_t)(2 * (r & 15))) & 63u;
-            const uint32_t vv =
-                funnel(valid32[(r >> 5) + 1], valid32[r >> 5], (uint32_t)(r & 31));
-            const uint32_t aa = ((vv & 7u) == 7u) ? s_lut[x] : (uint32_t)'X';
-            w[kk >> 2] |= aa << (8 * (kk & 3));
-          }
-        }
-        uint8_t* dst = a.pep + qbase + 16 * (uint64_t)c;
-        if (c >= n_pc) {
-        } else if (kk0 == 0 && kk1 == 16) {
-          *reinterpret_cast<uint4*>(dst) = make_uint4(w[0], w[1], w[2], w[3]);
-        } else {
-#pragma unroll
-          for (int kk = 0; kk < 16; ++kk)
-            if (kk >= kk0 && kk < kk1) dst[kk] = (uint8_t)(w[kk >> 2] >> (8 * (kk & 3)));
+        for (int q = 0; q < 4; ++q) {
+          const int nb = min(max(s - 4 * q, 0), 4);  // bytes of word q from segment 1
+          const uint32_t keep = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+          w[q] = (w[q] & keep) | (v[q] & ~keep);
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    d = dn;
-    rows = rn;
+  } else {
+    int jj = j;
+    for (int kk = kk0; kk < kk1; ++kk) {
+      const int q = q_first + kk;
+      while ((int64_t)q >= L.tp[jj + 1]) ++jj;
+      const int r = (int)(L.tn[jj] + 3 * ((int64_t)q - L.tp[jj]));
+      const int cw = r >> 4;
+      const uint32_t x = funnel(codes[cw + 1], codes[cw], (uint32_t)(2 * (r & 15))) & 63u;
+      const uint32_t vv = funnel(valid32[(r >> 5) + 1], valid32[r >> 5], (uint32_t)(r & 31));
+      const uint32_t aa = ((vv & 7u) == 7u) ? s_lut[x] : (uint32_t)'X';
+      w[kk >> 2] |= aa << (8 * (kk & 3));
+    }
+  }
+  uint8_t* const pdst = a.pep + g.qbase + 16 * (uint64_t)c;
+  if (kk0 == 0 && kk1 == 16) {
+    *reinterpret_cast<uint4*>(pdst) = make_uint4(w[0], w[1], w[2], w[3]);
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk)
+      if (kk >= kk0 && kk < kk1) pdst[kk] = (uint8_t)(w[kk >> 2] >> (8 * (kk & 3)));
   }
 }
 
@@ -539,8 +534,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
 
 void launch_extract(const ExtractArgs& a, hipStream_t s) {
   if (a.n_tiles == 0) return;
-  const uint32_t need = (a.n_tiles + kWaves - 1) / kWaves;
-  const uint32_t grid = min(need, a.grid ? a.grid : need);
+  const uint32_t grid = (a.n_tiles + kWaves - 1) / kWaves;  // one tile per wave
   hipLaunchKernelGGL(extract_kernel, dim3(grid), dim3(kThreads), 0, s, a);
 }
 
