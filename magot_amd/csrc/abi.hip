@@ -44,8 +44,9 @@ struct magot_genome {
   magot_ctx* ctx = nullptr;
   void* arena = nullptr;
   uint64_t arena_bytes = 0;
-  uint32_t* codes = nullptr;
+  uint32_t* codes = nullptr;  // forward then reverse-strand plane (ExtractArgs::span)
   uint32_t* lower = nullptr;
+  uint64_t span = 0;
   ExcRun* runs = nullptr;
   uint32_t* dir = nullptr;
   std::vector<uint64_t> contig_base, contig_len;
@@ -161,11 +162,16 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
     set_error("magot_genome_load: too many exception runs");
     return MAGOT_ERR_ARG;
   }
+  if (2 * hp.codes.size() * 4 + 16 > 0xFFFFFFFFull) {  // 32-bit buffer offsets (extract.hip)
+    set_error("magot_genome_load: genome above 8 Gbases is not supported");
+    return MAGOT_ERR_ARG;
+  }
   std::unique_ptr<magot_genome> g(new magot_genome());
   g->ctx = ctx;
   Carve cv;
-  uint64_t o_codes = cv.take<uint32_t>(hp.codes.size());
-  uint64_t o_lower = cv.take<uint32_t>(hp.lower.size());
+  // forward + reverse-strand planes, 4 words of slack for window over-reads
+  uint64_t o_codes = cv.take<uint32_t>(2 * hp.codes.size() + 4);
+  uint64_t o_lower = cv.take<uint32_t>(2 * hp.lower.size() + 4);
   uint64_t o_runs = cv.take<ExcRun>(hp.runs.size());
   uint64_t o_dir = cv.take<uint32_t>(hp.dir.size());
   MAGOT_HIP_TRY(hipMalloc(&g->arena, cv.used));
@@ -177,6 +183,12 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
   g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
   MAGOT_HIP_TRY(hipMemcpy(g->codes, hp.codes.data(), hp.codes.size() * 4, hipMemcpyHostToDevice));
   MAGOT_HIP_TRY(hipMemcpy(g->lower, hp.lower.data(), hp.lower.size() * 4, hipMemcpyHostToDevice));
+  MAGOT_HIP_TRY(hipMemset(g->codes + 2 * hp.codes.size(), 0, 16));
+  MAGOT_HIP_TRY(hipMemset(g->lower + 2 * hp.lower.size(), 0, 16));
+  launch_mirror_planes(g->codes, g->lower, hp.span, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  g->span = hp.span;
   MAGOT_HIP_TRY(hipMemcpy(g->runs, hp.runs.data(), hp.runs.size() * sizeof(ExcRun),
                           hipMemcpyHostToDevice));
   MAGOT_HIP_TRY(hipMemcpy(g->dir, hp.dir.data(), hp.dir.size() * 4, hipMemcpyHostToDevice));
@@ -387,6 +399,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   ExtractArgs& a = p->args;
   a.codes = g->codes;
   a.lower = g->lower;
+  a.span = g->span;
   a.runs = g->runs;
   a.dir = g->dir;
   a.ex_g = reinterpret_cast<const uint64_t*>(base + o_exg);
@@ -403,8 +416,6 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   a.total_pep = P;
   a.n_tiles = n_tiles;
   a.outputs = outputs;
-  a.grid = (uint32_t)(ctx->n_cu > 0 && ctx->blocks_per_cu > 0 ? ctx->n_cu * ctx->blocks_per_cu : 0);
-  if (const char* gb = std::getenv("MAGOT_GRID_BLOCKS")) a.grid = (uint32_t)std::atoi(gb);
   if (const char* dbg = std::getenv("MAGOT_DEBUG_PATHS")) {
     const int v = std::atoi(dbg);
     if (v & 1) a.outputs |= kDebugSlowNuc;

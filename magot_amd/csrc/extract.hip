@@ -125,6 +125,7 @@ struct Planes {
   const uint32_t* __restrict__ lower;
   const uint32_t* __restrict__ dir;
   const ExcRun* __restrict__ runs;
+  uint64_t span;
 };
 
 // Codes / soft-mask bits of the 16 genome bases starting at wbase.
@@ -170,8 +171,9 @@ __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
     while ((int)X.z <= pos) X = ex[++i];
     const int j0 = pos - p;
     const int n = min((int)X.z, end) - pos;
-    const uint64_t A = (uint64_t)X.x | ((uint64_t)X.y << 32);
     const bool rc = (X.w & kFlagRc) != 0;
+    const uint64_t U = (uint64_t)X.x | ((uint64_t)X.y << 32);
+    const uint64_t A = rc ? 2 * a.span - 1 - U : U;  // forward-strand anchor
     uint64_t glo, ghi, wbase;
     if (!rc) {
       glo = A + (uint64_t)pos;
@@ -197,13 +199,15 @@ __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
   return o;
 }
 
-// Wave-wide inclusive prefix sum.
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v, int lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t u = __shfl_up(v, d, 64);
-    if (lane >= d) v += u;
-  }
+// Wave-wide inclusive prefix sum with DPP row shifts and row broadcasts
+// (gfx9 wave64: row_shr:1/2/4/8 inside rows of 16, then row_bcast:15/31).
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
   return v;
 }
 
@@ -279,7 +283,7 @@ __device__ __forceinline__ TileGeom geom(const ExtractArgs& a, const TileDesc& d
 // (histogram of first chunks + wave prefix scan).
 __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* valid32,
                                       const TileDesc& d, const TileGeom& g, const TileRows& rows,
-                                      int lane) {
+                                      uint64_t span, int lane) {
   const int m = (int)d.m, nt = (int)d.nt;
 #pragma unroll
   for (int h = 0; h < 3; ++h) codes[lane + 64 * h] = 0;
@@ -294,10 +298,12 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
       const uint64_t gs = gw & ~(kRcBit | kExcBit);
       const int64_t s = (int64_t)(o0 - d.T0);
       const int64_t e = (int64_t)(o1 - d.T0);
-      const uint64_t A = rc ? gs + (o1 - o0) - 1 + (uint64_t)s : gs - (uint64_t)s;
+      // chunk byte p of the tile reads unified base U + p: forward g = gs + (p - s),
+      // reverse strand 2*span-1 - (gs + len-1 - (p - s))
+      const uint64_t U = rc ? 2 * span - gs - (o1 - o0) - (uint64_t)s : gs - (uint64_t)s;
       const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
       const uint32_t fl = (rc ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u);
-      L.ex[j] = make_uint4((uint32_t)A, (uint32_t)(A >> 32), end32, fl);
+      L.ex[j] = make_uint4((uint32_t)U, (uint32_t)(U >> 32), end32, fl);
       if (j >= 1) {
         const int cj = ((int)s + kChunk - 1) / kChunk;
         if (cj < g.n_all) atomicAdd(&codes[cj], 1u);
@@ -318,8 +324,10 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
   const uint32_t h0 = codes[3 * lane], h1 = codes[3 * lane + 1], h2 = codes[3 * lane + 2];
   const uint32_t p0 = valid32[lane];
   const uint32_t c1 = h0 + h1, c2 = c1 + h2;
-  const uint32_t cx = wave_scan(c2, lane) - c2;
-  const uint32_t px = wave_scan(p0, lane);
+  // both scans in one: interval counts (<= kExonCap) low, record counts high
+  const uint32_t sc = wave_scan(c2 | (p0 << 16));
+  const uint32_t cx = (sc & 0xFFFFu) - c2;
+  const uint32_t px = sc >> 16;
   L.cmap[3 * lane] = (uint8_t)(cx + h0);
   L.cmap[3 * lane + 1] = (uint8_t)(cx + c1);
   L.cmap[3 * lane + 2] = (uint8_t)(cx + c2);
@@ -327,33 +335,44 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
   __builtin_amdgcn_wave_barrier();
 }
 
+// Two plane words holding unified base u: byte offset (u >> 4) * 4 for the
+// code plane (sh = 2), (u >> 5) * 4 for the soft-mask plane (sh = 3).  Planes
+// stay below 4 GiB (span < 8 Gbases, checked at genome load), so offsets are 32-bit (one
+// alignbit + and) and the load is a raw buffer load off a scalar descriptor.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* plane) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(plane), (short)0, (int)0xFFFFFFFFu,
+                                           0x00020000);
+}
+
+__device__ __forceinline__ uint2 load_window(__amdgpu_buffer_rsrc_t plane, uint64_t u,
+                                             uint32_t sh) {
+  const uint32_t off = __builtin_amdgcn_alignbit((uint32_t)(u >> 32), (uint32_t)u, sh) & ~3u;
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(plane, off, 0, 0);
+  return make_uint2(v[0], v[1]);
+}
+
 // Fast-path chunk assembly from prefetched windows (branch-free in the
 // strand and segment count; see meta bits in extract_kernel).
+// Fast-path chunk assembly from prefetched windows: both segments read their
+// strand's plane forward, so this is two funnel shifts and a masked merge.
 __device__ __forceinline__ void fast_chunk(uint2 cA, uint2 lA, uint2 cB, uint2 lB, uint32_t mt,
                                            uint32_t& cw, uint32_t& lw) {
-  const uint32_t sa = (mt >> 8) & 31u;
-  uint32_t t1 = funnel(cA.y, cA.x, 2 * (sa & 15));
-  uint32_t l1 = funnel(lA.y, lA.x, sa) & 0xFFFFu;
-  const uint32_t t1r = ~rev_pairs(t1), l1r = __builtin_bitreverse32(l1) >> 16;
-  t1 = (mt & 2u) ? t1r : t1;
-  l1 = (mt & 2u) ? l1r : l1;
-  const uint32_t sb = (mt >> 16) & 31u;
-  uint32_t t2 = funnel(cB.y, cB.x, 2 * (sb & 15));
-  uint32_t l2 = funnel(lB.y, lB.x, sb) & 0xFFFFu;
-  const uint32_t t2r = ~rev_pairs(t2), l2r = __builtin_bitreverse32(l2) >> 16;
-  t2 = (mt & 8u) ? t2r : t2;
-  l2 = (mt & 8u) ? l2r : l2;
+  const uint32_t sa = (mt >> 8) & 31u, sb = (mt >> 16) & 31u;
+  const uint32_t t1 = funnel(cA.y, cA.x, 2 * (sa & 15));
+  const uint32_t l1 = funnel(lA.y, lA.x, sa);
+  const uint32_t t2 = funnel(cB.y, cB.x, 2 * (sb & 15));
+  const uint32_t l2 = funnel(lB.y, lB.x, sb);
   // n1 = bytes from segment A (16 when the chunk is one segment)
   const uint32_t n1 = (mt >> 24) & 31u;
   const uint32_t m2 = n1 >= 16 ? 0xFFFFFFFFu : ((1u << (2 * n1)) - 1u);
-  const uint32_t m1 = n1 >= 16 ? 0xFFFFu : ((1u << n1) - 1u);
+  const uint32_t m1 = (1u << n1) - 1u;
   cw = (t1 & m2) | (t2 & ~m2);
-  lw = (l1 & m1) | (l2 & ~m1);
+  lw = ((l1 & m1) | (l2 & ~m1)) & 0xFFFFu;
 }
 
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   __shared__ WaveLds s_wave[kWaves];
-  __shared__ uint32_t s_lut[64];
+  __shared__ uint8_t s_lut[64];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -376,12 +395,13 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   if (t >= a.n_tiles) return;
   const TileDesc d = load_desc(a, t);
   const TileGeom g = geom(a, d);
-  stage(L, codes, valid32, d, g, load_rows(a, d, lane), lane);
+  stage(L, codes, valid32, d, g, load_rows(a, d, lane), a.span, lane);
   const uint64_t T0 = d.T0;
 
   // ---- nucleotide chunks: issue every window load first -------------------
+  const __amdgpu_buffer_rsrc_t codes_rs = plane_rsrc(a.codes), lower_rs = plane_rsrc(a.lower);
   uint2 cA[kLaneChunks], lA[kLaneChunks], cB[kLaneChunks], lB[kLaneChunks];
-  uint32_t meta[kLaneChunks];  // bit0 active, 1 rcA, 3 rcB, 4 slow, 8..12 shiftA,
+  uint32_t meta[kLaneChunks];  // bit0 active, 4 slow, 8..12 shiftA,
                                // 16..20 shiftB, 24..28 bytes from segment A
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) {
@@ -393,20 +413,19 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     const int cend = min(p + kChunk, g.lim);
     const uint64_t A = (uint64_t)X.x | ((uint64_t)X.y << 32);
     const uint64_t B2 = (uint64_t)Y.x | ((uint64_t)Y.y << 32);
-    const bool rcA = (X.w & kFlagRc) != 0, rcB = (Y.w & kFlagRc) != 0;
     const int n1 = min((int)X.z, cend) - p;       // bytes of segment A (1..16)
     const bool two = n1 < cend - p;
-    const uint64_t wa = rcA ? A - (uint64_t)p - 15 : A + (uint64_t)p;
-    const uint64_t wb = two ? (rcB ? B2 - (uint64_t)p - 15 : B2 + (uint64_t)p) : wa;
+    const uint64_t wa = A + (uint64_t)p;
+    const uint64_t wb = two ? B2 + (uint64_t)p : wa;
     const bool slow = ((X.w | (two ? Y.w : 0u)) & kFlagExc) != 0 || (two && (int)Y.z < cend) ||
                       (a.outputs & kDebugSlowNuc);
-    meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (rcA ? 2u : 0u) | (rcB ? 8u : 0u) |
-              (slow ? 16u : 0u) | ((uint32_t)(wa & 31) << 8) | ((uint32_t)(wb & 31) << 16) |
+    meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (slow ? 16u : 0u) |
+              ((uint32_t)(wa & 31) << 8) | ((uint32_t)(wb & 31) << 16) |
               ((uint32_t)(two ? n1 : 16) << 24);
-    cA[k] = *reinterpret_cast<const uint2*>(a.codes + (wa >> 4));
-    lA[k] = *reinterpret_cast<const uint2*>(a.lower + (wa >> 5));
-    cB[k] = *reinterpret_cast<const uint2*>(a.codes + (wb >> 4));
-    lB[k] = *reinterpret_cast<const uint2*>(a.lower + (wb >> 5));
+    cA[k] = load_window(codes_rs, wa, 2);
+    lA[k] = load_window(lower_rs, wa, 3);
+    cB[k] = load_window(codes_rs, wb, 2);
+    lB[k] = load_window(lower_rs, wb, 3);
   }
   uint32_t cwk[kLaneChunks], lwk[kLaneChunks];
 #pragma unroll
@@ -422,7 +441,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     uint32_t ex = 0;
     uint32_t lit[4] = {0u, 0u, 0u, 0u};
     if (__builtin_amdgcn_readfirstlane(__ballot(slow_any != 0) != 0) && (mt & 17u) == 17u) {
-      const Planes pl{a.codes, a.lower, a.dir, a.runs};
+      const Planes pl{a.codes, a.lower, a.dir, a.runs, a.span};
       const Chunk o = build_chunk_slow(pl, p, g.lim, L.cmap[c], L.ex);
       cwk[k] = o.codes;
       lwk[k] = o.low;
@@ -490,10 +509,21 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
         const uint32_t idx = ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
                                               : funnel(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
                              63u;
-        const int vb = 3 * k;
-        const uint32_t okb = vb < 32 ? (ok0 >> vb) : (ok1 >> (vb - 32));
-        const uint32_t aa = (okb & 1u) ? s_lut[idx] : (uint32_t)'X';
-        v[k >> 2] |= aa << (8 * (k & 3));
+        v[k >> 2] |= (uint32_t)s_lut[idx] << (8 * (k & 3));
+      }
+      // residues whose codon holds a non-ACGT base become 'X'.  Bit 3k of
+      // (bad1:bad0) flags residue k; spread each word's 4 flags to byte masks.
+      const uint32_t bad0 = ~ok0 & 0x49249249u;  // residues 0..10
+      const uint32_t bad1 = ~ok1 & 0x00002492u;  // residues 11..15 (bits 3k-32)
+      if (__builtin_amdgcn_ballot_w64((bad0 | bad1) != 0)) {
+        const uint32_t f[4] = {bad0 & 0xFFFu, (bad0 >> 12) & 0xFFFu,
+                               ((bad0 >> 24) | (bad1 << 8)) & 0xFFFu, (bad1 >> 4) & 0xFFFu};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          // bits 0,3,6,9 -> 0,8,16,24 (partial products never collide)
+          const uint32_t m = ((f[q] * 0x8421u) & 0x01010101u) * 0xFFu;
+          v[q] = (v[q] & ~m) | (0x58585858u & m);
+        }
       }
       if (seg == 0) {
 #pragma unroll
@@ -530,7 +560,23 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void mirror_planes_kernel(uint32_t* __restrict__ codes,
+                                                            uint32_t* __restrict__ lower,
+                                                            uint64_t nw) {
+  // reverse-strand word w holds the complement of forward word nw-1-w, reversed
+  const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w < nw) codes[nw + w] = ~rev_pairs(codes[nw - 1 - w]);
+  if (w < nw / 2) lower[nw / 2 + w] = __builtin_bitreverse32(lower[nw / 2 - 1 - w]);
+}
+
 }  // namespace
+
+void launch_mirror_planes(uint32_t* codes, uint32_t* lower, uint64_t span, hipStream_t s) {
+  const uint64_t nw = span / 16;
+  if (nw == 0) return;
+  hipLaunchKernelGGL(mirror_planes_kernel, dim3((uint32_t)((nw + 255) / 256)), dim3(256), 0, s,
+                     codes, lower, nw);
+}
 
 void launch_extract(const ExtractArgs& a, hipStream_t s) {
   if (a.n_tiles == 0) return;

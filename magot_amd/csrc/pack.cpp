@@ -95,8 +95,9 @@ void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, H
   }
   out->extent = cur;
   const uint64_t padded = cur + 64;
-  out->codes.assign(padded / 16 + 4, 0u);
-  out->lower.assign(padded / 32 + 4, 0u);
+  out->span = (padded + 64 + 31) & ~31ull;
+  out->codes.assign(out->span / 16, 0u);
+  out->lower.assign(out->span / 32, 0u);
 
   // Split [0, extent) into 32-aligned pieces for the worker threads.
   unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
