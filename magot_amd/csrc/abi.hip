@@ -44,8 +44,7 @@ struct magot_genome {
   magot_ctx* ctx = nullptr;
   void* arena = nullptr;
   uint64_t arena_bytes = 0;
-  uint32_t* codes = nullptr;  // forward then reverse-strand plane (ExtractArgs::span)
-  uint32_t* lower = nullptr;
+  uint32_t* nib = nullptr;  // forward then reverse-strand nibble plane (ExtractArgs::span)
   uint64_t span = 0;
   ExcRun* runs = nullptr;
   uint32_t* dir = nullptr;
@@ -162,30 +161,26 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
     set_error("magot_genome_load: too many exception runs");
     return MAGOT_ERR_ARG;
   }
-  if (2 * hp.codes.size() * 4 + 16 > 0xFFFFFFFFull) {  // 32-bit buffer offsets (extract.hip)
-    set_error("magot_genome_load: genome above 8 Gbases is not supported");
+  if (2 * hp.nib.size() * 4 + 16 > 0xFFFFFFFFull) {  // 32-bit buffer offsets (extract.hip)
+    set_error("magot_genome_load: genomes above 4 Gbases are not supported");
     return MAGOT_ERR_ARG;
   }
   std::unique_ptr<magot_genome> g(new magot_genome());
   g->ctx = ctx;
   Carve cv;
   // forward + reverse-strand planes, 4 words of slack for window over-reads
-  uint64_t o_codes = cv.take<uint32_t>(2 * hp.codes.size() + 4);
-  uint64_t o_lower = cv.take<uint32_t>(2 * hp.lower.size() + 4);
+  uint64_t o_nib = cv.take<uint32_t>(2 * hp.nib.size() + 4);
   uint64_t o_runs = cv.take<ExcRun>(hp.runs.size());
   uint64_t o_dir = cv.take<uint32_t>(hp.dir.size());
   MAGOT_HIP_TRY(hipMalloc(&g->arena, cv.used));
   g->arena_bytes = cv.used;
   char* base = static_cast<char*>(g->arena);
-  g->codes = reinterpret_cast<uint32_t*>(base + o_codes);
-  g->lower = reinterpret_cast<uint32_t*>(base + o_lower);
+  g->nib = reinterpret_cast<uint32_t*>(base + o_nib);
   g->runs = reinterpret_cast<ExcRun*>(base + o_runs);
   g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
-  MAGOT_HIP_TRY(hipMemcpy(g->codes, hp.codes.data(), hp.codes.size() * 4, hipMemcpyHostToDevice));
-  MAGOT_HIP_TRY(hipMemcpy(g->lower, hp.lower.data(), hp.lower.size() * 4, hipMemcpyHostToDevice));
-  MAGOT_HIP_TRY(hipMemset(g->codes + 2 * hp.codes.size(), 0, 16));
-  MAGOT_HIP_TRY(hipMemset(g->lower + 2 * hp.lower.size(), 0, 16));
-  launch_mirror_planes(g->codes, g->lower, hp.span, ctx->stream);
+  MAGOT_HIP_TRY(hipMemcpy(g->nib, hp.nib.data(), hp.nib.size() * 4, hipMemcpyHostToDevice));
+  MAGOT_HIP_TRY(hipMemset(g->nib + 2 * hp.nib.size(), 0, 16));
+  launch_mirror_planes(g->nib, hp.span, ctx->stream);
   MAGOT_HIP_TRY(hipGetLastError());
   MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   g->span = hp.span;
@@ -397,8 +392,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   MAGOT_HIP_TRY(up(o_tq, tile_q.data(), tile_q.size() * 8));
 
   ExtractArgs& a = p->args;
-  a.codes = g->codes;
-  a.lower = g->lower;
+  a.nib = g->nib;
   a.span = g->span;
   a.runs = g->runs;
   a.dir = g->dir;

@@ -32,11 +32,12 @@ struct ExcRun {
 static_assert(sizeof(ExcRun) == 16, "ExcRun must be 16 bytes");
 
 struct HostPacked {
-  // Forward planes over [0, span) bases; span is a multiple of 32 with >= 64
-  // bases of zero padding past the last contig.  The device mirrors them
-  // into reverse-strand planes (mirror_planes) right after these words.
-  std::vector<uint32_t> codes;    // 16 bases per word, base i at bits 2*(i&15)
-  std::vector<uint32_t> lower;    // 32 bases per word, 1 = soft-masked (lowercase)
+  // Forward nibble plane over [0, span) bases (span: multiple of 32 with >= 64
+  // bases of zero padding past the last contig).  Base g is nibble g & 7 of
+  // word g >> 3: bits 0-1 code (A C G T = 0..3), bit 2 soft-masked
+  // (lower-case), bit 3 exception (byte kept in `runs`, code bits 0).  The
+  // device mirrors it into the reverse-strand plane (mirror_planes).
+  std::vector<uint32_t> nib;
   uint64_t span = 0;
   std::vector<ExcRun> runs;       // sorted by start, sentinel appended
   std::vector<uint32_t> dir;      // per 4096-block first run with end > block start
@@ -76,10 +77,9 @@ constexpr uint32_t kDebugPrologueOnly = 1u << 11;  // timing only: stop after st
 // ranges of the nucleotide output of at most kTile bytes, cut shorter where
 // they would touch more than kExonCap intervals or kTxCap records.
 struct ExtractArgs {
-  // Code / soft-mask planes in unified coordinates: [0, span) forward strand,
-  // [span, 2*span) reverse strand: u = 2*span-1-g is the complement of base g.
-  const uint32_t* codes;
-  const uint32_t* lower;
+  // Nibble plane in unified coordinates: [0, span) forward strand, [span,
+  // 2*span) reverse strand, where u = 2*span-1-g holds the complement of g.
+  const uint32_t* nib;
   uint64_t span;
   const ExcRun* runs;
   const uint32_t* dir;
@@ -102,8 +102,8 @@ struct ExtractArgs {
 
 void launch_extract(const ExtractArgs& a, hipStream_t s);
 int extract_blocks_per_cu();
-// Fill the reverse-strand halves of the code / soft-mask planes.
-void launch_mirror_planes(uint32_t* codes, uint32_t* lower, uint64_t span, hipStream_t s);
+// Fill the reverse-strand half of the nibble plane.
+void launch_mirror_planes(uint32_t* nib, uint64_t span, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Raw sequence batch ops (seqops.hip)

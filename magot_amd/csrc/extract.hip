@@ -51,20 +51,12 @@ struct WaveLds {
 constexpr uint32_t kFlagRc = 1u;
 constexpr uint32_t kFlagExc = 2u;
 
-__device__ __forceinline__ uint32_t rev_pairs(uint32_t x) {
-  // reverse the order of the sixteen 2-bit fields of x
-  x = __builtin_bitreverse32(x);
-  return ((x >> 1) & 0x55555555u) | ((x & 0x55555555u) << 1);
-}
-
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
   return __builtin_amdgcn_alignbit(hi, lo, sh);  // (hi:lo >> sh)[31:0], sh in 0..31
 }
 
-__device__ __forceinline__ uint32_t spread_codes(uint32_t c8) {
-  // four 2-bit codes -> four bytes 0..3
-  const uint32_t x = c8 | (c8 << 6);
-  return (x | (x << 12)) & 0x03030303u;
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+  return (a & mask) | (b & ~mask);  // v_bfi_b32 / v_bitop3
 }
 
 __device__ __forceinline__ uint32_t spread_bits(uint32_t m4) {
@@ -78,9 +70,10 @@ __device__ __forceinline__ uint32_t rc_literal(uint32_t b) {
   return (b == 'n' || b == 'N' || b == '-') ? b : (uint32_t)'n';
 }
 
+// Sixteen output bytes as nibbles (chunk byte k = nibble k of x0:x1), the
+// exception bytes among them and their literal values.
 struct Chunk {
-  uint32_t codes;   // 16 x 2-bit, byte k at bits 2k (already complemented for rc)
-  uint32_t low;     // 16 x soft-mask bit
+  uint32_t x0, x1;  // nibbles: code | lower << 2 | exception << 3
   uint32_t exc;     // 16 x "literal byte" bit
   uint32_t lit[4];  // literal bytes, little-endian by chunk byte
 };
@@ -98,17 +91,24 @@ __device__ __forceinline__ void put_literal(Chunk& o, int ka, int kb, uint32_t b
   }
 }
 
-// 16 bytes of ASCII: 'ACGT' for codes 0..3, lower-case where the soft-mask
-// bit is set (selector bit 2 picks the 'acgt' source), literal bytes patched.
-__device__ __forceinline__ uint4 chunk_ascii(uint32_t codes, uint32_t low, uint32_t exc,
+// Eight nibbles -> two words of selector bytes (one nibble per byte).
+__device__ __forceinline__ void spread_nibbles(uint32_t x, uint32_t& s0, uint32_t& s1) {
+  const uint32_t lo = x & 0x0F0F0F0Fu;          // nibbles 0 2 4 6
+  const uint32_t hi = (x >> 4) & 0x0F0F0F0Fu;   // nibbles 1 3 5 7
+  s0 = __builtin_amdgcn_perm(hi, lo, 0x05010400u);
+  s1 = __builtin_amdgcn_perm(hi, lo, 0x07030602u);
+}
+
+// 16 bytes of ASCII: selector bit 2 (soft mask) picks the 'acgt' half of the
+// table; exception bytes (selector >= 8) are patched from the literal words.
+__device__ __forceinline__ uint4 chunk_ascii(uint32_t x0, uint32_t x1, uint32_t exc,
                                              const uint32_t lit[4]) {
+  uint32_t s[4];
+  spread_nibbles(x0, s[0], s[1]);
+  spread_nibbles(x1, s[2], s[3]);
   uint32_t w[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t sel = spread_codes((codes >> (8 * q)) & 0xFFu) |
-                         (spread_bits((low >> (4 * q)) & 0xFu) << 2);
-    w[q] = __builtin_amdgcn_perm(0x74676361u, 0x54474341u, sel);
-  }
+  for (int q = 0; q < 4; ++q) w[q] = __builtin_amdgcn_perm(0x74676361u, 0x54474341u, s[q]);
   if (exc) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -120,24 +120,33 @@ __device__ __forceinline__ uint4 chunk_ascii(uint32_t codes, uint32_t low, uint3
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// 16 nibbles -> 16 packed 2-bit codes (base k at bits 2k) for translation.
+__device__ __forceinline__ uint32_t pack_codes(uint32_t x0, uint32_t x1) {
+  // per byte: code(2k) | code(2k+1) << 2 in the low nibble (high nibble junk)
+  const uint32_t y0 = bfi(0x03030303u, x0, x0 >> 2), y1 = bfi(0x03030303u, x1, x1 >> 2);
+  // bytes 0 and 2: four codes each
+  const uint32_t z0 = bfi(0x0F0F0F0Fu, y0, y0 >> 4), z1 = bfi(0x0F0F0F0Fu, y1, y1 >> 4);
+  return __builtin_amdgcn_perm(z1, z0, 0x06040200u);
+}
+
 struct Planes {
-  const uint32_t* __restrict__ codes;
-  const uint32_t* __restrict__ lower;
+  const uint32_t* __restrict__ nib;
   const uint32_t* __restrict__ dir;
   const ExcRun* __restrict__ runs;
   uint64_t span;
 };
 
-// Codes / soft-mask bits of the 16 genome bases starting at wbase.
-__device__ __forceinline__ void window(const Planes& a, uint64_t wbase, uint32_t& t,
-                                       uint32_t& lt) {
-  const uint2 c = *reinterpret_cast<const uint2*>(a.codes + (wbase >> 4));
-  const uint2 l = *reinterpret_cast<const uint2*>(a.lower + (wbase >> 5));
-  t = funnel(c.y, c.x, (uint32_t)(2 * (wbase & 15)));
-  lt = funnel(l.y, l.x, (uint32_t)(wbase & 31)) & 0xFFFFu;
+// Nibbles of the 16 unified bases starting at u.
+__device__ __forceinline__ void window(const uint32_t* nib, uint64_t u, uint32_t& x0,
+                                       uint32_t& x1) {
+  const uint32_t* w = nib + (u >> 3);
+  const uint32_t sh = 4u * (uint32_t)(u & 7);
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+  x0 = funnel(w1, w0, sh);
+  x1 = funnel(w2, w1, sh);
 }
 
-// Patch literal bytes of genome interval [glo, ghi] (chunk bytes from j0).
+// Patch literal bytes of forward genome interval [glo, ghi] (chunk bytes from j0).
 __device__ __forceinline__ void patch_runs(const Planes& a, uint64_t glo, uint64_t ghi, bool rc,
                                            int j0, Chunk& o) {
   const uint32_t d0 = a.dir[glo >> kDirShift];
@@ -160,8 +169,8 @@ __device__ __forceinline__ void patch_runs(const Planes& a, uint64_t glo, uint64
 __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
                                                const uint4* ex) {
   Chunk o;
-  o.codes = 0;
-  o.low = 0;
+  o.x0 = 0;
+  o.x1 = 0;
   o.exc = 0;
   o.lit[0] = o.lit[1] = o.lit[2] = o.lit[3] = 0;
   const int end = min(p + kChunk, lim);
@@ -173,27 +182,17 @@ __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
     const int n = min((int)X.z, end) - pos;
     const bool rc = (X.w & kFlagRc) != 0;
     const uint64_t U = (uint64_t)X.x | ((uint64_t)X.y << 32);
-    const uint64_t A = rc ? 2 * a.span - 1 - U : U;  // forward-strand anchor
-    uint64_t glo, ghi, wbase;
-    if (!rc) {
-      glo = A + (uint64_t)pos;
-      ghi = glo + (uint64_t)(n - 1);
-      wbase = glo;
-    } else {
-      ghi = A - (uint64_t)pos;
-      glo = ghi - (uint64_t)(n - 1);
-      wbase = ghi - 15;
+    uint32_t x0, x1;
+    window(a.nib, U + (uint64_t)p, x0, x1);  // chunk byte k <- unified base U + p + k
+    const uint64_t m = (n >= 16 ? ~0ull : ((1ull << (4 * n)) - 1ull)) << (4 * j0);
+    o.x0 = bfi((uint32_t)m, x0, o.x0);
+    o.x1 = bfi((uint32_t)(m >> 32), x1, o.x1);
+    if (X.w & kFlagExc) {
+      // forward coordinates of chunk bytes j0 .. j0+n-1
+      const uint64_t u0 = U + (uint64_t)pos;
+      const uint64_t glo = rc ? 2 * a.span - 1 - (u0 + (uint64_t)(n - 1)) : u0;
+      patch_runs(a, glo, glo + (uint64_t)(n - 1), rc, j0, o);
     }
-    uint32_t t, lt;
-    window(a, wbase, t, lt);
-    if (rc) {
-      t = ~rev_pairs(t);
-      lt = __builtin_bitreverse32(lt) >> 16;
-    }
-    const uint32_t m2 = (n >= 16 ? 0xFFFFFFFFu : ((1u << (2 * n)) - 1u)) << (2 * j0);
-    o.codes |= (t << (2 * j0)) & m2;
-    o.low |= (lt << j0) & (((1u << n) - 1u) << j0);
-    if (X.w & kFlagExc) patch_runs(a, glo, ghi, rc, j0, o);
     pos += n;
   }
   return o;
@@ -335,39 +334,35 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
   __builtin_amdgcn_wave_barrier();
 }
 
-// Two plane words holding unified base u: byte offset (u >> 4) * 4 for the
-// code plane (sh = 2), (u >> 5) * 4 for the soft-mask plane (sh = 3).  Planes
-// stay below 4 GiB (span < 8 Gbases, checked at genome load), so offsets are 32-bit (one
-// alignbit + and) and the load is a raw buffer load off a scalar descriptor.
+// Three plane words holding unified bases u .. u+15 at byte offset (u >> 3) * 4.
+// The plane stays below 4 GiB (genome < 4 Gbases, checked at genome load), so
+// the offset is 32-bit (one alignbit + and) and the load is a raw buffer
+// load off a scalar descriptor.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* plane) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(plane), (short)0, (int)0xFFFFFFFFu,
-                                           0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(plane), (short)0,
+                                           (int)0xFFFFFFFFu, 0x00020000);
 }
 
-__device__ __forceinline__ uint2 load_window(__amdgpu_buffer_rsrc_t plane, uint64_t u,
-                                             uint32_t sh) {
-  const uint32_t off = __builtin_amdgcn_alignbit((uint32_t)(u >> 32), (uint32_t)u, sh) & ~3u;
-  const auto v = __builtin_amdgcn_raw_buffer_load_b64(plane, off, 0, 0);
-  return make_uint2(v[0], v[1]);
+__device__ __forceinline__ uint3 load_window(__amdgpu_buffer_rsrc_t plane, uint64_t u) {
+  const uint32_t off = __builtin_amdgcn_alignbit((uint32_t)(u >> 32), (uint32_t)u, 1) & ~3u;
+  const auto v = __builtin_amdgcn_raw_buffer_load_b96(plane, off, 0, 0);
+  return make_uint3(v[0], v[1], v[2]);
 }
 
-// Fast-path chunk assembly from prefetched windows (branch-free in the
-// strand and segment count; see meta bits in extract_kernel).
 // Fast-path chunk assembly from prefetched windows: both segments read their
-// strand's plane forward, so this is two funnel shifts and a masked merge.
-__device__ __forceinline__ void fast_chunk(uint2 cA, uint2 lA, uint2 cB, uint2 lB, uint32_t mt,
-                                           uint32_t& cw, uint32_t& lw) {
-  const uint32_t sa = (mt >> 8) & 31u, sb = (mt >> 16) & 31u;
-  const uint32_t t1 = funnel(cA.y, cA.x, 2 * (sa & 15));
-  const uint32_t l1 = funnel(lA.y, lA.x, sa);
-  const uint32_t t2 = funnel(cB.y, cB.x, 2 * (sb & 15));
-  const uint32_t l2 = funnel(lB.y, lB.x, sb);
+// strand's half of the plane forward, so this is two funnel shifts per
+// segment and a masked merge at nibble n1.
+__device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, uint32_t& x0,
+                                           uint32_t& x1) {
+  const uint32_t sa = (mt >> 6) & 28u, sb = (mt >> 14) & 28u;  // 4 * (u & 7)
+  const uint32_t a0 = funnel(A.y, A.x, sa), a1 = funnel(A.z, A.y, sa);
+  const uint32_t b0 = funnel(B.y, B.x, sb), b1 = funnel(B.z, B.y, sb);
   // n1 = bytes from segment A (16 when the chunk is one segment)
   const uint32_t n1 = (mt >> 24) & 31u;
-  const uint32_t m2 = n1 >= 16 ? 0xFFFFFFFFu : ((1u << (2 * n1)) - 1u);
-  const uint32_t m1 = (1u << n1) - 1u;
-  cw = (t1 & m2) | (t2 & ~m2);
-  lw = ((l1 & m1) | (l2 & ~m1)) & 0xFFFFu;
+  const uint32_t mlo = n1 >= 8 ? 0xFFFFFFFFu : ((1u << (4 * n1)) - 1u);
+  const uint32_t mhi = n1 >= 16 ? 0xFFFFFFFFu : (n1 <= 8 ? 0u : ((1u << (4 * (n1 - 8))) - 1u));
+  x0 = bfi(mlo, a0, b0);
+  x1 = bfi(mhi, a1, b1);
 }
 
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
@@ -399,10 +394,10 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   const uint64_t T0 = d.T0;
 
   // ---- nucleotide chunks: issue every window load first -------------------
-  const __amdgpu_buffer_rsrc_t codes_rs = plane_rsrc(a.codes), lower_rs = plane_rsrc(a.lower);
-  uint2 cA[kLaneChunks], lA[kLaneChunks], cB[kLaneChunks], lB[kLaneChunks];
-  uint32_t meta[kLaneChunks];  // bit0 active, 4 slow, 8..12 shiftA,
-                               // 16..20 shiftB, 24..28 bytes from segment A
+  const __amdgpu_buffer_rsrc_t nib_rs = plane_rsrc(a.nib);
+  uint3 wA[kLaneChunks], wB[kLaneChunks];
+  uint32_t meta[kLaneChunks];  // bit0 active, 4 slow, 8..10 u_A & 7, 16..18 u_B & 7,
+                               // 24..28 bytes from segment A
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) {
     const int c = min(lane + 64 * k, g.n_all - 1);  // clamped: inactive lanes redo a chunk
@@ -411,28 +406,27 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     const uint4 X = L.ex[i];
     const uint4 Y = L.ex[min(i + 1, (int)d.m - 1)];
     const int cend = min(p + kChunk, g.lim);
-    const uint64_t A = (uint64_t)X.x | ((uint64_t)X.y << 32);
-    const uint64_t B2 = (uint64_t)Y.x | ((uint64_t)Y.y << 32);
-    const int n1 = min((int)X.z, cend) - p;       // bytes of segment A (1..16)
+    const uint64_t UA = (uint64_t)X.x | ((uint64_t)X.y << 32);
+    const uint64_t UB = (uint64_t)Y.x | ((uint64_t)Y.y << 32);
+    const int n1 = min((int)X.z, cend) - p;  // bytes of segment A (1..16)
     const bool two = n1 < cend - p;
-    const uint64_t wa = A + (uint64_t)p;
-    const uint64_t wb = two ? B2 + (uint64_t)p : wa;
+    const uint64_t wa = UA + (uint64_t)p;
+    const uint64_t wb = two ? UB + (uint64_t)p : wa;
     const bool slow = ((X.w | (two ? Y.w : 0u)) & kFlagExc) != 0 || (two && (int)Y.z < cend) ||
                       (a.outputs & kDebugSlowNuc);
     meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (slow ? 16u : 0u) |
-              ((uint32_t)(wa & 31) << 8) | ((uint32_t)(wb & 31) << 16) |
+              ((uint32_t)(wa & 7) << 8) | ((uint32_t)(wb & 7) << 16) |
               ((uint32_t)(two ? n1 : 16) << 24);
-    cA[k] = load_window(codes_rs, wa, 2);
-    lA[k] = load_window(lower_rs, wa, 3);
-    cB[k] = load_window(codes_rs, wb, 2);
-    lB[k] = load_window(lower_rs, wb, 3);
+    wA[k] = load_window(nib_rs, wa);
+    wB[k] = load_window(nib_rs, wb);
   }
-  uint32_t cwk[kLaneChunks], lwk[kLaneChunks];
+  uint32_t x0k[kLaneChunks], x1k[kLaneChunks];
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) fast_chunk(cA[k], lA[k], cB[k], lB[k], meta[k], cwk[k], lwk[k]);
+  for (int k = 0; k < kLaneChunks; ++k) fast_chunk(wA[k], wB[k], meta[k], x0k[k], x1k[k]);
   uint32_t slow_any = 0;
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) slow_any |= meta[k] & 16u;
+  const bool any_slow = __builtin_amdgcn_readfirstlane(__ballot(slow_any != 0) != 0);
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) {
     const int c = lane + 64 * k;
@@ -440,11 +434,11 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     const uint32_t mt = meta[k];
     uint32_t ex = 0;
     uint32_t lit[4] = {0u, 0u, 0u, 0u};
-    if (__builtin_amdgcn_readfirstlane(__ballot(slow_any != 0) != 0) && (mt & 17u) == 17u) {
-      const Planes pl{a.codes, a.lower, a.dir, a.runs, a.span};
+    if (any_slow && (mt & 17u) == 17u) {
+      const Planes pl{a.nib, a.dir, a.runs, a.span};
       const Chunk o = build_chunk_slow(pl, p, g.lim, L.cmap[c], L.ex);
-      cwk[k] = o.codes;
-      lwk[k] = o.low;
+      x0k[k] = o.x0;
+      x1k[k] = o.x1;
       ex = o.exc;
       lit[0] = o.lit[0];
       lit[1] = o.lit[1];
@@ -453,9 +447,11 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     }
     if (mt & 1u) {
       if (want_nuc && c < g.n_out)
-        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) = chunk_ascii(cwk[k], lwk[k], ex, lit);
-      codes[c] = cwk[k];
-      valid16[c] = (uint16_t)~ex;
+        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) = chunk_ascii(x0k[k], x1k[k], ex, lit);
+      if (want_pep) {
+        codes[c] = pack_codes(x0k[k], x1k[k]);
+        valid16[c] = (uint16_t)~ex;
+      }
     }
   }
   if (!want_pep || g.n_res <= 0) return;
@@ -560,22 +556,23 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void mirror_planes_kernel(uint32_t* __restrict__ codes,
-                                                            uint32_t* __restrict__ lower,
+__global__ __launch_bounds__(256) void mirror_planes_kernel(uint32_t* __restrict__ nib,
                                                             uint64_t nw) {
-  // reverse-strand word w holds the complement of forward word nw-1-w, reversed
+  // reverse-strand word w: forward word nw-1-w with its nibbles reversed and
+  // the codes complemented (soft-mask and exception bits kept)
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (w < nw) codes[nw + w] = ~rev_pairs(codes[nw - 1 - w]);
-  if (w < nw / 2) lower[nw / 2 + w] = __builtin_bitreverse32(lower[nw / 2 - 1 - w]);
+  if (w >= nw) return;
+  const uint32_t x = __builtin_bswap32(nib[nw - 1 - w]);
+  nib[nw + w] = (((x >> 4) & 0x0F0F0F0Fu) | ((x << 4) & 0xF0F0F0F0u)) ^ 0x33333333u;
 }
 
 }  // namespace
 
-void launch_mirror_planes(uint32_t* codes, uint32_t* lower, uint64_t span, hipStream_t s) {
-  const uint64_t nw = span / 16;
+void launch_mirror_planes(uint32_t* nib, uint64_t span, hipStream_t s) {
+  const uint64_t nw = span / 8;
   if (nw == 0) return;
   hipLaunchKernelGGL(mirror_planes_kernel, dim3((uint32_t)((nw + 255) / 256)), dim3(256), 0, s,
-                     codes, lower, nw);
+                     nib, nw);
 }
 
 void launch_extract(const ExtractArgs& a, hipStream_t s) {

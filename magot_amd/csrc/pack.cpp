@@ -1,5 +1,6 @@
-// Host-side genome packer: raw contig bytes -> 2-bit code plane, soft-mask
-// plane, exception runs and their block directory (layout: common.h).
+// Host-side genome packer: raw contig bytes -> nibble plane (2-bit code,
+// soft-mask bit, exception bit per base), exception runs and their block
+// directory (layout: common.h).
 //
 // The bytes packed are exactly what GenomeSequence keeps (genome.py:870-877):
 // every byte of every sequence line except CR/LF, case preserved.  ACGTacgt
@@ -15,22 +16,19 @@ namespace magot {
 namespace {
 
 struct ByteClass {
-  uint8_t code[256];
-  uint8_t lower[256];
+  uint8_t nib[256];    // nibble for ACGTacgt, 8 (exception) otherwise
   uint8_t plain[256];  // 1 for ACGTacgt
   ByteClass() {
     for (int i = 0; i < 256; ++i) {
-      code[i] = 0;
-      lower[i] = 0;
+      nib[i] = 8;
       plain[i] = 0;
     }
     const char up[4] = {'A', 'C', 'G', 'T'};
     for (int c = 0; c < 4; ++c) {
-      code[(uint8_t)up[c]] = (uint8_t)c;
+      nib[(uint8_t)up[c]] = (uint8_t)c;
       plain[(uint8_t)up[c]] = 1;
-      code[(uint8_t)(up[c] | 0x20)] = (uint8_t)c;
+      nib[(uint8_t)(up[c] | 0x20)] = (uint8_t)(c | 4);
       plain[(uint8_t)(up[c] | 0x20)] = 1;
-      lower[(uint8_t)(up[c] | 0x20)] = 1;
     }
   }
 };
@@ -40,10 +38,10 @@ const ByteClass& byte_class() {
   return k;
 }
 
-// Pack global coordinates [p0, p1) (p0, p1 multiples of 32, so no code or
-// mask word is shared with another piece).
+// Pack global coordinates [p0, p1) (p0, p1 multiples of 32, so no plane word
+// is shared with another piece).
 void pack_piece(const uint8_t* const* seqs, const HostPacked& layout, uint64_t p0, uint64_t p1,
-                uint32_t* codes, uint32_t* lower, std::vector<ExcRun>* runs) {
+                uint32_t* nib, std::vector<ExcRun>* runs) {
   const ByteClass& bc = byte_class();
   const auto& base = layout.contig_base;
   const auto& len = layout.contig_len;
@@ -61,9 +59,8 @@ void pack_piece(const uint8_t* const* seqs, const HostPacked& layout, uint64_t p
     const uint8_t* s = seqs[c] + (lo - cb);
     for (uint64_t g = lo; g < hi; ++g) {
       uint8_t b = *s++;
+      nib[g >> 3] |= (uint32_t)bc.nib[b] << (4 * (g & 7));
       if (bc.plain[b]) {
-        codes[g >> 4] |= (uint32_t)bc.code[b] << (2 * (g & 15));
-        lower[g >> 5] |= (uint32_t)bc.lower[b] << (g & 31);
         if (open) {
           runs->push_back(cur);
           open = false;
@@ -96,8 +93,7 @@ void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, H
   out->extent = cur;
   const uint64_t padded = cur + 64;
   out->span = (padded + 64 + 31) & ~31ull;
-  out->codes.assign(out->span / 16, 0u);
-  out->lower.assign(out->span / 32, 0u);
+  out->nib.assign(out->span / 8, 0u);
 
   // Split [0, extent) into 32-aligned pieces for the worker threads.
   unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
@@ -113,7 +109,7 @@ void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, H
       if (k >= npieces) return;
       uint64_t p0 = k * step, p1 = std::min(cur, p0 + step);
       if (p0 < p1)
-        pack_piece(seqs, *out, p0, p1, out->codes.data(), out->lower.data(), &piece_runs[k]);
+        pack_piece(seqs, *out, p0, p1, out->nib.data(), &piece_runs[k]);
     }
   };
   unsigned nthreads = (unsigned)std::min<uint64_t>(hw, npieces);
