@@ -116,7 +116,17 @@ def cpu_baseline(w, budget_bases):
     for r in recs:
         mo.get_fasta(r, aset, 'protein')
     t2 = time.perf_counter()
-    return {'value': bases / (t2 - t0), 'unit': 'bases/s', 'cores': 1, 'kind': 'port',
+    rate = bases / (t2 - t0)
+    cal = None
+    cal_path = os.path.join(ROOT, 'profiles', 'cpu_calibration.json')
+    if os.path.exists(cal_path):
+        with open(cal_path) as fh:
+            ratio = json.load(fh)['port_over_reference_mean']
+        # the reference's own loop (AnnotationSet.__getitem__ evals, genome.py:536-544)
+        # runs this much slower than the port on the same input (scripts/calibrate_cpu.py)
+        cal = {'reference_equivalent_bases_per_s': rate / ratio, 'port_over_reference': ratio,
+               'source': 'profiles/cpu_calibration.json'}
+    return {'value': rate, 'unit': 'bases/s', 'cores': 1, 'kind': 'port', 'calibration': cal,
             'sample': '%d of %d transcripts (every %d-th), %d CDS bases; get_fasta nucleotide '
                       '%.2fs + protein %.2fs; pure-Python restatement of the reference loop '
                       '(oracle/magot_oracle.py)' % (len(recs), w.n_tx, step, bases, t1 - t0,

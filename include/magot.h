@@ -93,10 +93,12 @@ int magot_ctx_create(int device, magot_ctx** out);
 void magot_ctx_destroy(magot_ctx* ctx);
 
 /*
- * Pack a genome into HBM: 2-bit codes (ACGT, case-folded), a 1-bit soft-mask
- * plane, and a run list of every other byte (N, IUPAC, '-', spaces ...) with a
+ * Pack a genome into HBM: a nibble plane (2-bit ACGT code, soft-mask bit,
+ * exception bit per base) plus its reverse-complement mirror, and a run list
+ * of every byte that is not ACGTacgt (N, IUPAC, '-', spaces ...) with a
  * 4096-base directory.  seqs[i] points at lens[i] raw bytes of contig i,
- * exactly the bytes genome.py:875 keeps (every byte except CR/LF).
+ * exactly the bytes genome.py:875 keeps (every byte except CR/LF).  Genomes
+ * up to 4 Gbases per device (MAGOT_ERR_ARG above).
  * Replaces: GenomeSequence (genome.py:854-877) as the data the path reads.
  */
 int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
@@ -107,8 +109,8 @@ int magot_genome_stats(const magot_genome* g, uint64_t* total_bases, uint64_t* n
 void magot_genome_destroy(magot_genome* g);
 
 /*
- * Build a device-resident plan: interval table -> output offsets, 12 KiB
- * output tiles, per-tile exon and record ranges, all uploaded to HBM.
+ * Build a device-resident plan: interval table -> output offsets, ~3 KiB
+ * wave tiles, per-tile exon and record ranges, all uploaded to HBM.
  * nuc_bytes / pep_bytes receive the total output sizes (pep_bytes counts the
  * untrimmed frame-0 translation, floor(len/3) per record; the single leading
  * 'X' trim of genome.py:819-821 is applied by the caller on fetch).
