@@ -414,8 +414,6 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     const int v = std::atoi(dbg);
     if (v & 1) a.outputs |= kDebugSlowNuc;
     if (v & 2) a.outputs |= kDebugSlowPep;
-    if (v & 4) a.outputs |= kDebugNoLoads;
-    if (v & 8) a.outputs |= kDebugPrologueOnly;
   }
   uint8_t lut[64];
   standard_lut(lut);

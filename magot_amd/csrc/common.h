@@ -69,8 +69,6 @@ constexpr uint64_t kExcBit = 1ull << 62;      // interval touches an exception r
 // force the general per-segment / per-residue paths.
 constexpr uint32_t kDebugSlowNuc = 1u << 8;
 constexpr uint32_t kDebugSlowPep = 1u << 9;
-constexpr uint32_t kDebugNoLoads = 1u << 10;     // timing only: skip genome plane loads
-constexpr uint32_t kDebugPrologueOnly = 1u << 11;  // timing only: stop after staging
 
 // Device plan.  Zero-length intervals and records without a codon are
 // compacted away on the host (they add no output); tiles are 16-byte aligned

@@ -291,3 +291,36 @@ def test_c3_full_size_vs_c_oracle():
     """The headline workload (1 Gb genome, 500k transcripts), byte for byte."""
     w = synth.make('C3')
     check_against_oracle(w)
+
+
+@pytest.mark.parametrize('paths', ['1', '2', '3'])
+def test_forced_general_paths_vs_c_oracle(monkeypatch, paths):
+    """MAGOT_DEBUG_PATHS routes every chunk (1), every residue chunk (2) or
+    both (3) through the general per-segment / per-residue code."""
+    monkeypatch.setenv('MAGOT_DEBUG_PATHS', paths)
+    w = synth.make('small', seed=11, genome_bases=2_000_000, n_tx=800, iupac_rate=1e-3)
+    check_against_oracle(w)
+
+
+def test_sorted_record_order_vs_c_oracle():
+    w = synth.make('small', seed=12, genome_bases=3_000_000, n_tx=1500, iupac_rate=1e-3,
+                   order='sorted')
+    check_against_oracle(w)
+
+
+def test_degenerate_intervals_vs_c_oracle():
+    """Zero-length intervals, records shorter than one codon, 1-2 base
+    exons mixed with long ones, and intervals clamped at contig ends."""
+    rng = np.random.default_rng(13)
+    w = synth.make('small', seed=13, genome_bases=1_000_000, n_tx=600, iupac_rate=2e-3)
+    n = w.n_exons
+    pick = rng.random(n)
+    w.ex_len = np.where(pick < 0.08, 0, np.where(pick < 0.16, rng.integers(1, 3, size=n),
+                                                  w.ex_len)).astype(np.int64)
+    # last interval of the first 20 records runs past its contig end (slice clamp)
+    last = np.cumsum(w.ex_count)[:20] - 1
+    clen = w.contig_len[w.tx_contig[:20]]
+    w.ex_start = w.ex_start.copy()
+    w.ex_start[last] = np.maximum(clen - 3, w.ex_start[last])
+    w.ex_len[last] = 10
+    check_against_oracle(w)
