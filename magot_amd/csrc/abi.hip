@@ -305,46 +305,61 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   }
 
   // --- tiles ----------------------------------------------------------------
-  // residues whose codon starts before output byte T (monotone pointer jq)
-  uint64_t jq = 0;
-  auto pcount = [&](uint64_t T) -> uint64_t {
-    while (jq < Tc && tn[jq + 1] <= T) ++jq;
-    if (jq >= Tc) return P;
-    if (tn[jq] > T) return tp[jq];                           // before the first record
-    const uint64_t into = T - tn[jq];
-    return tp[jq] + std::min((into + 2) / 3, tp[jq + 1] - tp[jq]);
+  // A tile owns nucleotide bytes [T0, T1) and residues [R0, R1).  Residue
+  // ownership is rounded up to 16-residue (16-byte) store chunks, so nearly
+  // every peptide store is a full aligned chunk; the residues a tile owns past
+  // its last codon start are decoded from its kHalo bytes of look-ahead.
+  auto pcount = [&](uint64_t T) -> uint64_t {  // residues whose codon starts before T
+    const uint64_t j = std::upper_bound(tn.begin(), tn.begin() + Tc, T) - tn.begin();
+    if (j == 0) return 0;
+    const uint64_t into = T - tn[j - 1];
+    return tp[j - 1] + std::min((into + 2) / 3, tp[j] - tp[j - 1]);
+  };
+  auto rec_of = [&](uint64_t q) -> uint64_t {  // compacted record holding residue q < P
+    return (std::upper_bound(tp.begin(), tp.begin() + Tc, q) - tp.begin()) - 1;
   };
   std::vector<uint64_t> tile_start, tile_q;
   std::vector<uint32_t> tile_ex, tile_tx;
-  uint64_t e1 = 0, e2 = 0, j1 = 0, j2 = 0;
-  uint64_t T0 = 0;
-  uint64_t Q0 = pcount(0);
+  uint64_t e1 = 0, e2 = 0;
+  uint64_t T0 = 0, R0 = 0;
   while (T0 < B) {
     while (e1 < Ec && ex_out[e1 + 1] <= T0) ++e1;           // interval containing T0
-    while (j1 < Tc && tp[j1 + 1] <= Q0) ++j1;               // record holding residue Q0
+    const uint64_t j1 = R0 < P ? rec_of(R0) : Tc;            // record holding residue R0
     uint64_t T1 = std::min<uint64_t>(T0 + kTile, B);
     if (e1 + kExonCap < Ec) T1 = std::min<uint64_t>(T1, ex_out[e1 + kExonCap] - kHalo);
-    if (j1 + kTxCap < Tc) T1 = std::min<uint64_t>(T1, tn[j1 + kTxCap]);
+    if (j1 + kTxCap - kChunk < Tc) T1 = std::min<uint64_t>(T1, tn[j1 + kTxCap - kChunk]);
     if (T1 < B) T1 &= ~(uint64_t)(kChunk - 1);
     if (T1 < T0 + kChunk) T1 = std::min<uint64_t>(T0 + kChunk, B);
-    const uint64_t Q1 = pcount(T1);
     const uint64_t dec_end = std::min<uint64_t>(T1 + kHalo, B);
+    // residues owned: every codon starting before T1, rounded up to a chunk,
+    // but only codons that end inside the decoded range and at most 64 chunks
+    uint64_t R1 = P;
+    if (T1 < B) {
+      R1 = std::min<uint64_t>((pcount(T1) + kChunk - 1) & ~(uint64_t)(kChunk - 1), P);
+      R1 = std::min<uint64_t>(R1, pcount(dec_end - 2));
+      R1 = std::min<uint64_t>(R1, (R0 & ~(uint64_t)(kChunk - 1)) + 64 * kChunk);
+    }
+    if (R1 < R0) R1 = R0;
     if (e2 < e1) e2 = e1;
     while (e2 < Ec && ex_out[e2] < dec_end) ++e2;           // intervals touching the decode range
-    if (j2 < j1) j2 = j1;
-    while (j2 < Tc && tp[j2] < Q1) ++j2;                    // records holding residues [Q0, Q1)
-    if (e2 - e1 > (uint64_t)kExonCap || (Q1 > Q0 && j2 - j1 > (uint64_t)kTxCap)) {
+    const uint64_t j2 = R1 > R0 ? rec_of(R1 - 1) + 1 : j1;  // records holding residues [R0, R1)
+    if (e2 - e1 > (uint64_t)kExonCap || (R1 > R0 && j2 - j1 > (uint64_t)kTxCap) ||
+        (R1 > R0 && tn[rec_of(R1 - 1)] + 3 * (R1 - 1 - tp[rec_of(R1 - 1)]) + 3 > dec_end)) {
       set_error("magot_plan_create: internal tiling error");
       return MAGOT_ERR_STATE;
     }
     tile_start.push_back(T0);
-    tile_q.push_back(Q0);
+    tile_q.push_back(R0);
     tile_ex.push_back((uint32_t)e1);
     tile_ex.push_back((uint32_t)e2);
-    tile_tx.push_back((uint32_t)j1);
-    tile_tx.push_back((uint32_t)(Q1 > Q0 ? j2 : j1));
+    tile_tx.push_back((uint32_t)(R1 > R0 ? j1 : 0));
+    tile_tx.push_back((uint32_t)(R1 > R0 ? j2 : 0));
     T0 = T1;
-    Q0 = Q1;
+    R0 = R1;
+  }
+  if (R0 != P) {
+    set_error("magot_plan_create: internal tiling error (residues)");
+    return MAGOT_ERR_STATE;
   }
   tile_start.push_back(B);
   tile_q.push_back(P);

@@ -59,7 +59,8 @@ constexpr int kLaneChunks = 3;                // chunk slots per lane per tile
 constexpr int kSlots = 64 * kLaneChunks;      // 192 chunk slots per wave tile
 constexpr int kTile = 189 * kChunk;           // 3024 output bytes per tile: <= 1008 residues,
                                               // so <= 64 residue chunks (one per lane)
-constexpr int kHalo = kChunk;                 // codons may run 2 bytes past the tile
+constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
+                                              // the residues rounded up to a 16-byte store
 constexpr int kExonCap = 128;                 // intervals staged in LDS per tile
 constexpr int kTxCap = 64;                    // records staged in LDS per tile
 constexpr int kPepSlots = 64;                 // residue chunks per tile

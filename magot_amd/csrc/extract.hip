@@ -12,25 +12,26 @@
 //
 // Work decomposition (output-stationary, HBM-bound):
 //   * The host cuts the concatenated nucleotide output into 16-byte aligned
-//     tiles of <= 3056 bytes (191 chunks of 16 bytes; shorter where a tile
+//     tiles of <= 3024 bytes (189 chunks of 16 bytes; shorter where a tile
 //     would touch more than kExonCap intervals or kTxCap records).  A tile
-//     belongs to ONE wavefront: 64 lanes x 3 chunk slots = 191 output chunks
-//     + 1 halo chunk (codons may run 2 bytes past the tile), so there are no
-//     workgroup barriers; waves are persistent and prefetch the next tile's
-//     descriptors and interval/record rows while the current tile computes.
-//   * Staging: the tile's intervals go to wave-private LDS as {64-bit genome
+//     belongs to ONE wavefront: 64 lanes x 3 chunk slots (189 output chunks +
+//     a halo chunk for codons that run past the tile end), so the only
+//     workgroup barrier is the one publishing the codon table.
+//   * Staging: the tile's intervals go to wave-private LDS as {64-bit unified
 //     anchor, tile-relative end, flags}; chunk -> interval and residue chunk
-//     -> record maps come from an LDS histogram + wave prefix scan.
-//   * A chunk is at most two interval segments on the fast path: each is a
-//     16-base window of the 2-bit code plane and the soft-mask plane (one
-//     dwordx2 load each), reversed in-register for '-' intervals (bit reverse,
-//     pair swap, complement), merged by mask, turned into ASCII with one
-//     v_perm per 4 bytes, and stored with one 16-byte store.  Intervals that
-//     touch an exception run (N, IUPAC ...; flagged per interval by the host)
-//     and chunks over 3+ intervals take a per-segment path.
-//   * Codes and validity bits stay in LDS; a residue chunk funnel-shifts 48
-//     bases of codes out of LDS per record segment (<= 2 on the fast path),
-//     looks the 16 codons up in an LDS table and stores 16 bytes.
+//     -> record maps come from an LDS histogram + one packed DPP wave scan.
+//   * The genome is a nibble plane (code | soft-mask << 2 | exception << 3)
+//     followed by its reverse-complement mirror, so a '-' interval reads its
+//     strand forward exactly like a '+' interval.  A chunk is at most two
+//     interval segments on the fast path: one buffer_load_dwordx3 window per
+//     segment, two funnel shifts, a nibble-mask merge, v_perm nibble spread +
+//     v_perm ASCII table, one 16-byte store.  Intervals that touch an
+//     exception run (N, IUPAC ...; flagged per interval by the host) and
+//     chunks over 3+ intervals take build_chunk_slow.
+//   * 2-bit codes and validity bits of the tile stay in LDS; a residue chunk
+//     funnel-shifts 48 bases of codes out of LDS per record segment (<= 2 on
+//     the fast path), looks the 16 codons up in a 64-byte LDS table and
+//     stores 16 bytes.
 #include "common.h"
 
 namespace magot {

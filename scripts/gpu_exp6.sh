@@ -12,5 +12,5 @@ run() {  # name order outputs
 }
 run sorted sorted nuc+pep
 run random random nuc+pep
-run nuc sorted nuc
-run pep sorted pep
+run nuc random nuc
+run pep random pep
