@@ -53,6 +53,12 @@ def dist_setup(n_gpus):
     return dist, rank, local, world
 
 
+def shard_seed(config, rank):
+    """Seed of rank `rank`'s shard: SURVEY 8(d) seed for rank 0, +1000 per rank."""
+    from magot_amd import synth
+    return synth.SEED_BASE + {'C2': 2, 'C3': 3, 'C5': 5, 'small': 9}[config] + 1000 * rank
+
+
 def barrier(dist):
     if dist is not None:
         dist.barrier()
@@ -152,8 +158,7 @@ def main():
     from magot_amd import _lib, engine, synth
 
     t0 = time.perf_counter()
-    seed = synth.SEED_BASE + {'C2': 2, 'C3': 3, 'C5': 5}[args.config] + 1000 * rank
-    w = synth.make(args.config, seed=seed)
+    w = synth.make(args.config, seed=shard_seed(args.config, rank))
     t_gen = time.perf_counter() - t0
     log('generated %s shard: %d contigs, %d transcripts, %d exons, %d CDS bases (%.1fs)'
         % (args.config, len(w.contig_len), w.n_tx, w.n_exons, w.cds_bases, t_gen))
