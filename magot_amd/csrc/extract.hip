@@ -482,56 +482,58 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   }
   uint32_t w[4] = {0u, 0u, 0u, 0u};
   if (!slow) {
-#pragma unroll 1
+    // 16 codon indices (6 bits each) and "all three bases plain" bits (bit 3k)
+    // of record j from r1 and of record j+1 from r2, merged at residue s, so
+    // the table lookups run once per lane whatever the segment count.
+    uint32_t Y[2][3], OK[2][2];
+#pragma unroll
     for (int seg = 0; seg < 2; ++seg) {
-      if (seg == 1 && !two) break;
-      const int r0 = seg == 0 ? r1 : r2;
+      const int r0 = (seg == 1 && two) ? r2 : r1;
       const int cw = r0 >> 4;
       const uint32_t sh = (uint32_t)(2 * (r0 & 15));
-      const uint32_t X0 = codes[cw], X1 = codes[cw + 1], X2 = codes[cw + 2], X3 = codes[cw + 3],
-                     X4 = codes[cw + 4];
-      const uint32_t Y[4] = {funnel(X1, X0, sh), funnel(X2, X1, sh), funnel(X3, X2, sh),
-                             funnel(X4, X3, sh)};
+      const uint32_t X0 = codes[cw], X1 = codes[cw + 1], X2 = codes[cw + 2], X3 = codes[cw + 3];
+      Y[seg][0] = funnel(X1, X0, sh);
+      Y[seg][1] = funnel(X2, X1, sh);
+      Y[seg][2] = funnel(X3, X2, sh);
       const int vw = r0 >> 5;
       const uint32_t vsh = (uint32_t)(r0 & 31);
       const uint32_t V0 = valid32[vw], V1 = valid32[vw + 1], V2 = valid32[vw + 2];
       const uint32_t Z0 = funnel(V1, V0, vsh), Z1 = funnel(V2, V1, vsh);
-      // bit 3k of ok = all three bases of codon k are plain ACGT
-      const uint32_t ok0 = Z0 & funnel(Z1, Z0, 1) & funnel(Z1, Z0, 2);
-      const uint32_t ok1 = Z1 & (Z1 >> 1) & (Z1 >> 2);
-      uint32_t v[4] = {0u, 0u, 0u, 0u};
+      OK[seg][0] = Z0 & funnel(Z1, Z0, 1) & funnel(Z1, Z0, 2);
+      OK[seg][1] = Z1 & (Z1 >> 1) & (Z1 >> 2);
+    }
+    const int sc = min(s, 16);  // residues taken from record j
+    uint32_t Ym[3], ok0, ok1;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int ob = 6 * k;
-        const uint32_t idx = ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
-                                              : funnel(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
-                             63u;
-        v[k >> 2] |= (uint32_t)s_lut[idx] << (8 * (k & 3));
-      }
-      // residues whose codon holds a non-ACGT base become 'X'.  Bit 3k of
-      // (bad1:bad0) flags residue k; spread each word's 4 flags to byte masks.
-      const uint32_t bad0 = ~ok0 & 0x49249249u;  // residues 0..10
-      const uint32_t bad1 = ~ok1 & 0x00002492u;  // residues 11..15 (bits 3k-32)
-      if (__builtin_amdgcn_ballot_w64((bad0 | bad1) != 0)) {
-        const uint32_t f[4] = {bad0 & 0xFFFu, (bad0 >> 12) & 0xFFFu,
-                               ((bad0 >> 24) | (bad1 << 8)) & 0xFFFu, (bad1 >> 4) & 0xFFFu};
+    for (int q = 0; q < 3; ++q) {
+      const int nb = min(max(6 * sc - 32 * q, 0), 32);
+      Ym[q] = bfi(nb >= 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u), Y[0][q], Y[1][q]);
+    }
+    {
+      const int n0 = min(3 * sc, 32), n1 = max(3 * sc - 32, 0);
+      ok0 = bfi(n0 >= 32 ? 0xFFFFFFFFu : ((1u << n0) - 1u), OK[0][0], OK[1][0]);
+      ok1 = bfi((1u << n1) - 1u, OK[0][1], OK[1][1]);
+    }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          // bits 0,3,6,9 -> 0,8,16,24 (partial products never collide)
-          const uint32_t m = ((f[q] * 0x8421u) & 0x01010101u) * 0xFFu;
-          v[q] = (v[q] & ~m) | (0x58585858u & m);
-        }
-      }
-      if (seg == 0) {
+    for (int k = 0; k < 16; ++k) {
+      const int ob = 6 * k;
+      const uint32_t idx = ((ob & 31) <= 26 ? (Ym[ob >> 5] >> (ob & 31))
+                                            : funnel(Ym[(ob >> 5) + 1], Ym[ob >> 5], ob & 31)) &
+                           63u;
+      w[k >> 2] |= (uint32_t)s_lut[idx] << (8 * (k & 3));
+    }
+    // residues whose codon holds a non-ACGT base become 'X'.  Bit 3k of
+    // (bad1:bad0) flags residue k; spread each word's 4 flags to byte masks.
+    const uint32_t bad0 = ~ok0 & 0x49249249u;  // residues 0..10
+    const uint32_t bad1 = ~ok1 & 0x00002492u;  // residues 11..15 (bits 3k-32)
+    if (__builtin_amdgcn_ballot_w64((bad0 | bad1) != 0)) {
+      const uint32_t f[4] = {bad0 & 0xFFFu, (bad0 >> 12) & 0xFFFu,
+                             ((bad0 >> 24) | (bad1 << 8)) & 0xFFFu, (bad1 >> 4) & 0xFFFu};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) w[q] = v[q];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int nb = min(max(s - 4 * q, 0), 4);  // bytes of word q from segment 1
-          const uint32_t keep = nb >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-          w[q] = (w[q] & keep) | (v[q] & ~keep);
-        }
+      for (int q = 0; q < 4; ++q) {
+        // bits 0,3,6,9 -> 0,8,16,24 (partial products never collide)
+        const uint32_t m = ((f[q] * 0x8421u) & 0x01010101u) * 0xFFu;
+        w[q] = (w[q] & ~m) | (0x58585858u & m);
       }
     }
   } else {
