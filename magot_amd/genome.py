@@ -498,8 +498,8 @@ class BaseAnnotation(object):
             start, length = _slice_interval(contig, self.coords[0] - 1, self.coords[1])
             dev = batch.bind(seqs)
             return (dev.index[self.seqid], start, length, rc)
-        except NotImplementedError:
-            raise
+        except (NotImplementedError, engine.MagotError):
+            raise  # device / build failures are not reference semantics: fail loudly
         except Exception:
             _emit(_MSG_GETSEQ, self.seqid)
         return None

@@ -184,3 +184,19 @@ def test_cli_argument_parsing():
                                              'longest=True'])
     assert name == 'gff2fasta' and args == ['a.fa', 'b.gtf']
     assert kw == {'seq_type': 'protein', 'longest': 'True'}
+
+
+def test_no_device_fails_loudly(monkeypatch):
+    """Without a usable device the product path raises MagotError -- it never
+    falls back to a CPU path or degrades into the reference's diagnostics."""
+    from magot_amd import _lib
+
+    def no_device(*a, **k):
+        raise _lib.MagotError('no HIP device visible')
+    monkeypatch.setattr(G.engine, 'DeviceGenome', no_device)
+    g = G.Genome('>c1\nACGTACGTAC\n')
+    g.read_gff('c1\tx\tgene\t1\t9\t.\t+\t.\tID=g1\n'
+               'c1\tx\tmRNA\t1\t9\t.\t+\t.\tID=m1;Parent=g1\n'
+               'c1\tx\tCDS\t1\t9\t.\t+\t0\tID=c1;Parent=m1\n')
+    with pytest.raises(_lib.MagotError):
+        g.annotations.get_fasta('gene')
