@@ -38,7 +38,9 @@ enum magot_status {
   MAGOT_ERR_ARG = -1,      /* bad argument / inconsistent tables           */
   MAGOT_ERR_HIP = -2,      /* HIP runtime failure (no device, OOM, fault)   */
   MAGOT_ERR_RANGE = -3,    /* interval outside its contig                   */
-  MAGOT_ERR_STATE = -4     /* call out of order (e.g. fetch before execute) */
+  MAGOT_ERR_STATE = -4,    /* call out of order (e.g. fetch before execute) */
+  MAGOT_ERR_UNSUPPORTED = -5 /* input takes a reference diagnostic path: use the
+                                Python object path (magot_gff_plan)              */
 };
 
 /* Output selection for a plan (magot_plan_create.outputs). */
@@ -171,6 +173,38 @@ int magot_translate_sizes(const uint64_t* seq_off, uint64_t n, const int32_t* fr
 int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
                           const int32_t* frames, const uint8_t* strands, const uint8_t* lut64,
                           const uint64_t* pep_off, uint8_t* out);
+
+/*
+ * Native batch planner for gff2fasta (genome_tools.py:324-330).
+ * Parses GFF3/GTF text with read_gff's rules and default arguments
+ * (genome.py:242-415: '#'/8-tab acceptance, version sniffing, ID synthesis
+ * and de-duplication, v2 parent hierarchy, Base/Parent typing), keeps the
+ * AnnotationSet model (global ID lookup: last matching type in sorted order,
+ * genome.py:536-544) and lowers AnnotationSet.get_fasta(feature)
+ * (genome.py:578-582, 677-731; longest=False, genomic=False) to interval and
+ * record tables for magot_plan_create plus a FASTA text skeleton.
+ * seqids / contig_lens: the GenomeSequence (genome.py:854-877) in the order
+ * its contigs were given to magot_genome_load.  flags: MAGOT_GFF_PROTEIN for
+ * seq_type="protein", MAGOT_GFF_ORDER_PY2 for CPython 2.7 dict order.
+ * Returns MAGOT_ERR_UNSUPPORTED when the input would take one of the
+ * reference's diagnostic paths (prints, None, exceptions): the caller then
+ * uses the object path, which reproduces them.
+ */
+#define MAGOT_GFF_PROTEIN 1u
+#define MAGOT_GFF_ORDER_PY2 2u
+typedef struct magot_gffplan magot_gffplan;
+int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
+                   const uint64_t* contig_lens, uint32_t n_contigs, const char* feature,
+                   uint32_t flags, magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx);
+/* Copy the planned tables (n_exons / n_tx entries from magot_gff_plan). */
+int magot_gffplan_tables(const magot_gffplan* p, magot_exon* exons, magot_tx* txs);
+/* The FASTA text: skeleton + record payloads from magot_plan_fetch (nuc for
+ * nucleotide plans, untrimmed pep for protein; the leading-'X' trim of
+ * genome.py:819-821 is applied here).  out == NULL: *out_len = size only. */
+int magot_gffplan_render(const magot_gffplan* p, const uint8_t* nuc, const uint64_t* noff,
+                         const uint8_t* pep, const uint64_t* poff, uint8_t* out, uint64_t cap,
+                         uint64_t* out_len);
+void magot_gffplan_destroy(magot_gffplan* p);
 
 #ifdef __cplusplus
 }

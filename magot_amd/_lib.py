@@ -30,7 +30,12 @@ EXPORTS = (
     'magot_run', 'magot_plan_time', 'magot_plan_device_outputs',
     'magot_plan_algorithmic_bytes',
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
+    'magot_gff_plan', 'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
 )
+
+ERR_UNSUPPORTED = -5
+GFF_PROTEIN = 1
+GFF_ORDER_PY2 = 2
 
 
 class MagotError(RuntimeError):
@@ -74,6 +79,14 @@ def _declare(lib):
         'magot_translate_sizes': (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
         'magot_translate_batch': (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
                                                  _vp, _vp]),
+        'magot_gff_plan': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64,
+                                          ctypes.POINTER(ctypes.c_char_p), _u64p, ctypes.c_uint32,
+                                          ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(_vp),
+                                          _u64p, _u64p]),
+        'magot_gffplan_tables': (ctypes.c_int, [_vp, _vp, _vp]),
+        'magot_gffplan_render': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
+                                                _u64p]),
+        'magot_gffplan_destroy': (None, [_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -134,6 +134,63 @@ class ExtractionPlan(object):
             pass
 
 
+class GffPlan(object):
+    """Native gff2fasta planner (magot_gff_plan): GFF text -> interval and
+    record tables + FASTA skeleton.  ``GffPlan.build`` returns None when the
+    input takes one of the reference's diagnostic paths (the caller then uses
+    the object path).  Host-only: no device needed to plan or render."""
+
+    def __init__(self, handle, n_exons, n_tx, protein):
+        self.handle = handle
+        self.protein = protein
+        self.exons = np.zeros(n_exons, dtype=EXON_DTYPE)
+        self.txs = np.zeros(n_tx, dtype=TX_DTYPE)
+        check(_lib.lib().magot_gffplan_tables(handle, ptr(self.exons), ptr(self.txs)),
+              'magot_gffplan_tables')
+
+    @classmethod
+    def build(cls, gff, names, lengths, feature='gene', protein=False, order='insertion'):
+        L = _lib.lib()
+        text = _as_bytes(gff)
+        n = len(names)
+        arr = (ctypes.c_char_p * max(n, 1))(*[_as_bytes(x) for x in names])
+        lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+        flags = (_lib.GFF_PROTEIN if protein else 0) | \
+            (_lib.GFF_ORDER_PY2 if order == 'py2' else 0)
+        h = ctypes.c_void_p()
+        ne, nt = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = L.magot_gff_plan(text, len(text), arr, lens.ctypes.data_as(_lib._u64p), n,
+                              _as_bytes(feature), flags, ctypes.byref(h), ctypes.byref(ne),
+                              ctypes.byref(nt))
+        if rc == _lib.ERR_UNSUPPORTED:
+            return None
+        check(rc, 'magot_gff_plan')
+        return cls(h, ne.value, nt.value, protein)
+
+    def render(self, nuc, noff, pep, poff):
+        """The FASTA text (bytes) around the fetched record payloads."""
+        L = _lib.lib()
+        size = ctypes.c_uint64()
+        args = (ptr(nuc), ptr(noff), ptr(pep), ptr(poff))
+        check(L.magot_gffplan_render(self.handle, *args, None, 0, ctypes.byref(size)),
+              'magot_gffplan_render')
+        out = np.empty(size.value, dtype=np.uint8)
+        check(L.magot_gffplan_render(self.handle, *args, ptr(out), size.value,
+                                     ctypes.byref(size)), 'magot_gffplan_render')
+        return out.tobytes()
+
+    def close(self):
+        if self.handle:
+            _lib.lib().magot_gffplan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _concat(seqs):
     parts = [_as_bytes(s) for s in seqs]
     off = np.zeros(len(parts) + 1, dtype=np.uint64)
@@ -187,4 +244,4 @@ def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
 
 
 __all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'OUT_NUC',
-           'OUT_PEP', 'MagotError']
+           'OUT_PEP', 'MagotError', 'GffPlan']

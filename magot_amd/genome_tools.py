@@ -2,6 +2,7 @@
 
     python -m magot_amd.genome_tools gff2fasta <fasta> <gff> [seq_type=protein]
            [longest=True] [genomic=True] [from_exons=True] [order=py2|insertion]
+           [native=False]
     python -m magot_amd.genome_tools cds2pep <cds.fasta>
 
 Arguments follow the reference's CLI convention (genome_tools.py:25-45):
@@ -39,8 +40,19 @@ def _write(text):
 
 
 def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', longest='False',
-              genomic='False', order='py2'):
-    """genome_tools.py:324-330."""
+              genomic='False', order='py2', native='True'):
+    """genome_tools.py:324-330.
+
+    Default arguments go through the native planner (magot_gff_plan: read_gff
+    + get_fasta lowering in C++) and one kernel launch; inputs that take one
+    of the reference's diagnostic paths, and the longest / genomic /
+    from_exons variants, use the object path (``native=False`` forces it)."""
+    if (native == 'True' and from_exons != 'True' and _literal(longest) is False and
+            _literal(genomic) is False and seq_type in ('nucleotide', 'protein')):
+        text = _gff2fasta_native(genome_sequence, gff, seq_type, order)
+        if text is not None:
+            _write(text + '\n')
+            return
     g = genome.Genome(genome_sequence)
     if from_exons == 'True':
         # reference quirk kept: a str features_to_ignore is a substring test
@@ -50,6 +62,29 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
     text = g.annotations.get_fasta('gene', seq_type=seq_type, longest=_literal(longest),
                                    genomic=_literal(genomic), order=order)
     _write(text + '\n')
+
+
+def _gff2fasta_native(genome_sequence, gff, seq_type, order):
+    """The gff2fasta text via the native planner, or None when it declines."""
+    if order not in ('py2', 'insertion'):
+        raise ValueError("order must be 'insertion' or 'py2'")
+    seqs = genome.GenomeSequence(genome_sequence)
+    names = list(seqs)
+    protein = seq_type == 'protein'
+    plan = engine.GffPlan.build(genome.ensure_file(gff).read(), names,
+                                [len(seqs[n]) for n in names], protein=protein, order=order)
+    if plan is None:
+        return None
+    try:
+        ex = engine.ExtractionPlan(seqs.device(), plan.exons, plan.txs,
+                                   engine.OUT_PEP if protein else engine.OUT_NUC)
+        try:
+            nuc, noff, pep, poff = ex.run()
+        finally:
+            ex.close()
+        return plan.render(nuc, noff, pep, poff).decode('latin-1')
+    finally:
+        plan.close()
 
 
 def cds2pep(fasta_file):

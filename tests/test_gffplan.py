@@ -1,0 +1,152 @@
+"""Native gff2fasta planner (magot_gff_plan, csrc/gffplan.cpp) on CPU.
+
+The planner is host code: it parses the GFF with read_gff's rules, orders the
+gene records and lowers get_fasta to interval / record tables plus a text
+skeleton.  Here the record payloads are computed from those tables by the
+oracle (never by the product), and the rendered text must equal the oracle's
+gff2fasta output byte for byte (and hence the reference's goldens).  Inputs
+that take a reference diagnostic path must be declined (None) so that the
+object path, which reproduces the diagnostics, runs instead.
+"""
+
+import numpy as np
+import pytest
+
+import goldlib
+from magot_amd import engine, synth
+from magot_amd import genome as G
+from oracle import magot_oracle as mo
+
+
+def _payloads(plan, seqs):
+    """Record bytes for the plan's tables (oracle; untrimmed peptides)."""
+    nuc, pep, noff, poff = [], [], [0], [0]
+    ex, tx = plan.exons, plan.txs
+    for t in range(len(tx)):
+        b, n = int(tx['exon_begin'][t]), int(tx['n_exons'][t])
+        parts = []
+        for e in range(b, b + n):
+            st = int(ex['start_rc'][e])
+            rc = bool(st >> 63)
+            st &= (1 << 63) - 1
+            s = seqs[int(ex['contig'][e])][st:st + int(ex['len'][e])]
+            parts.append(mo.reverse_complement(s) if rc else s)
+        s = ''.join(parts)
+        nuc.append(s)
+        noff.append(noff[-1] + len(s))
+        p = mo.translate(s, trimX=False) if len(s) > 2 else ''
+        pep.append(p)
+        poff.append(poff[-1] + len(p))
+    enc = lambda parts: np.frombuffer((''.join(parts) + ' ').encode('latin-1'), np.uint8)
+    return enc(nuc), np.array(noff, np.uint64), enc(pep), np.array(poff, np.uint64)
+
+
+def native_gff2fasta(fasta, gff, seq_type='nucleotide', order='insertion'):
+    gs = G.GenomeSequence(fasta)
+    names = list(gs)
+    plan = engine.GffPlan.build(G.ensure_file(gff).read(), names, [len(gs[n]) for n in names],
+                                protein=seq_type == 'protein', order=order)
+    if plan is None:
+        return None
+    text = plan.render(*_payloads(plan, [gs[n] for n in names]))
+    plan.close()
+    return text.decode('latin-1') + '\n'
+
+
+CASES = [
+    ('obiroi', 'O.biroi_refseqGenomeSubset.fasta', 'O.biroi_NCBIrefseq_gff3Subset.gff'),
+    ('c14-gtf', None, 'StandardGTF.gtf'),
+    ('c14-transcriptless', None, 'transcriptlessGTF.gtf'),
+    ('c14-minimal-gff3', None, 'minimalGFF3.gff'),
+]
+
+
+@pytest.fixture(scope='module')
+def c14():
+    return goldlib.rebuild_c14()
+
+
+@pytest.mark.parametrize('name,fa,gff', CASES)
+@pytest.mark.parametrize('seq_type', ['nucleotide', 'protein'])
+@pytest.mark.parametrize('order', ['insertion', 'py2'])
+def test_native_plan_matches_oracle(c14, name, fa, gff, seq_type, order):
+    fasta = c14 if fa is None else goldlib.path(fa)
+    got = native_gff2fasta(fasta, goldlib.path(gff), seq_type, order)
+    if got is None:
+        # declined: the reference takes a diagnostic path on this input
+        out = []
+        try:
+            mo.gff2fasta(fasta, goldlib.path(gff), seq_type=seq_type, order=order, out=out)
+            diag = bool(out)
+        except Exception:
+            diag = True
+        assert diag, 'native planner declined an input without diagnostics'
+        return
+    want = mo.gff2fasta(fasta, goldlib.path(gff), seq_type=seq_type, order=order)
+    assert got == want
+
+
+def test_native_plan_reproduces_test_suite_goldens(c14):
+    """test_data/test_suite.py:12-13 cksums through the native planner."""
+    nuc = native_gff2fasta(c14, goldlib.path('StandardGTF.gtf'), 'nucleotide', 'py2')
+    pep = native_gff2fasta(c14, goldlib.path('StandardGTF.gtf'), 'protein', 'py2')
+    assert goldlib.posix_cksum(nuc.encode('latin-1')) == (2836090577, 690750)
+    assert goldlib.posix_cksum(pep.encode('latin-1')) == (111942461, 233762)
+
+
+@pytest.mark.parametrize('fmt', ['gff3', 'gtf'])
+def test_native_plan_synthetic(fmt):
+    w = synth.make('small', seed=21, genome_bases=400_000, n_tx=300, iupac_rate=1e-3)
+    fasta = w.fasta_text()
+    gff = w.gff3_text() if fmt == 'gff3' else w.gtf_text()
+    for seq_type in ('nucleotide', 'protein'):
+        got = native_gff2fasta(fasta, gff, seq_type, 'py2')
+        assert got is not None
+        assert got == mo.gff2fasta(fasta, gff, seq_type=seq_type, order='py2')
+
+
+@pytest.mark.parametrize('gff', [
+    # orphan parent (print + None in read_gff)
+    'c1\tx\tCDS\t1\t9\t.\t+\t0\tID=c1;Parent=nope\n',
+    # invalid strand on a CDS (print + TypeError in get_fasta)
+    'c1\tx\tgene\t1\t9\t.\t+\t.\tID=g1\nc1\tx\tmRNA\t1\t9\t.\t+\t.\tID=m1;Parent=g1\n'
+    'c1\tx\tCDS\t1\t9\t.\t?\t0\tID=c1;Parent=m1\n',
+    # missing seqid
+    'zz\tx\tgene\t1\t9\t.\t+\t.\tID=g1\nzz\tx\tmRNA\t1\t9\t.\t+\t.\tID=m1;Parent=g1\n'
+    'zz\tx\tCDS\t1\t9\t.\t+\t0\tID=c1;Parent=m1\n',
+    # non-integer coordinate (ValueError)
+    'c1\tx\tgene\t1\tten\t.\t+\t.\tID=g1\n',
+    # mixed Base / Parent children
+    'c1\tx\tgene\t1\t9\t.\t+\t.\tID=g1\nc1\tx\tCDS\t1\t9\t.\t+\t0\tID=c1;Parent=g1\n'
+    'c1\tx\tmRNA\t1\t9\t.\t+\t.\tID=m1;Parent=g1\n',
+])
+def test_native_plan_declines_diagnostic_paths(gff):
+    gs = G.GenomeSequence('>c1\nACGTACGTACGT\n')
+    assert engine.GffPlan.build(gff, list(gs), [12], protein=True) is None
+
+
+def test_native_plan_dedupe_and_join_shapes():
+    """Duplicate IDs (ID2, ID-3), genes without CDS (blank records), nested
+    parents and '-' strand ordering by the last child's strand."""
+    fasta = '>c1\n' + 'ACGTTGCAAC' * 30 + '\n>c2\n' + 'GGGAAATTTCCC' * 20 + '\n'
+    gff = ''.join([
+        'c1\tx\tgene\t1\t300\t.\t+\t.\tID=g1\n',
+        'c1\tx\tmRNA\t1\t300\t.\t+\t.\tID=m1;Parent=g1\n',
+        'c1\tx\tCDS\t10\t40\t.\t+\t0\tID=cds;Parent=m1\n',
+        'c1\tx\tCDS\t50\t90\t.\t+\t0\tID=cds;Parent=m1\n',
+        'c1\tx\tCDS\t100\t140\t.\t-\t0\tID=cds;Parent=m1\n',
+        'c1\tx\tmRNA\t1\t300\t.\t-\t.\tID=m2;Parent=g1\n',
+        'c1\tx\tCDS\t200\t260\t.\t-\t0\tID=m2c;Parent=m2\n',
+        'c1\tx\tCDS\t150\t180\t.\t-\t0\tID=m2d;Parent=m2\n',
+        'c1\tx\tCDS\t150\t180\t.\t-\t0\tID=m2e;Parent=m2\n',
+        'c2\tx\tgene\t1\t200\t.\t+\t.\tID=g2\n',
+        'c2\tx\tgene\t1\t200\t.\t+\t.\tID=g3\n',
+        'c2\tx\tmRNA\t5\t150\t.\t+\t.\tID=m3;Parent=g3\n',
+        'c2\tx\tCDS\t5\t150\t.\t+\t0\tID=m3c;Parent=m3\n',
+        'c2\tx\tCDS\t230\t260\t.\t+\t0\tID=past;Parent=m3\n',
+    ])
+    for seq_type in ('nucleotide', 'protein'):
+        for order in ('insertion', 'py2'):
+            got = native_gff2fasta(fasta, gff, seq_type, order)
+            assert got is not None
+            assert got == mo.gff2fasta(fasta, gff, seq_type=seq_type, order=order)

@@ -13,6 +13,7 @@ import pytest
 import goldlib
 from magot_amd import engine, synth
 from magot_amd import genome as G
+from oracle import magot_oracle as mo
 
 pytestmark = pytest.mark.gpu
 
@@ -203,6 +204,28 @@ def test_reference_test_suite_lines_12_13_14(c14_path):
     assert goldlib.posix_cksum(data) == (111942461, 233762)
     data = _cli(['cds2pep', goldlib.path('CDSannotations.cds')])
     assert goldlib.posix_cksum(data) == (111942461, 233762)
+
+
+@pytest.mark.parametrize('ann', ['StandardGTF.gtf', 'transcriptlessGTF.gtf', 'minimalGFF3.gff'])
+@pytest.mark.parametrize('seq_type', ['nucleotide', 'protein'])
+def test_cli_native_planner_equals_object_path(c14_path, ann, seq_type):
+    """gff2fasta through the native planner (default) and through the Python
+    object path (native=False) write identical bytes."""
+    base = ['gff2fasta', c14_path, goldlib.path(ann), 'seq_type=' + seq_type]
+    assert _cli(base) == _cli(base + ['native=False'])
+
+
+def test_cli_native_planner_synthetic(tmp_path):
+    w = synth.make('small', seed=31, genome_bases=2_000_000, n_tx=1000, iupac_rate=1e-3)
+    fa, gf = tmp_path / 'g.fa', tmp_path / 'a.gff3'
+    fa.write_text(w.fasta_text())
+    gf.write_text(w.gff3_text())
+    for seq_type in ('nucleotide', 'protein'):
+        base = ['gff2fasta', str(fa), str(gf), 'seq_type=' + seq_type]
+        native = _cli(base)
+        assert native == _cli(base + ['native=False'])
+        want = mo.gff2fasta(str(fa), str(gf), seq_type=seq_type, order='py2')
+        assert native == want.encode('latin-1')
 
 
 def test_synth_small_gpu():
