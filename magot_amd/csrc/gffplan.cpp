@@ -15,10 +15,14 @@
 // reproduces those diagnostics exactly.  This file never touches sequence
 // bytes: the extraction itself is the HIP kernel's.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
 #include <string>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -38,21 +42,111 @@ struct Feature {
 
 struct Table {
   std::string name;
-  std::vector<uint32_t> keys;                   // IDs in insertion order
-  std::unordered_map<uint32_t, uint32_t> slot;  // ID -> feature index
+  std::vector<uint32_t> keys;  // IDs in insertion order
 };
 
 struct Unsupported {};  // a diagnostic path of the reference: use the object path
 
+using sv = std::string_view;
+
+// Interned strings with stable storage (views stay valid as the pool grows),
+// found through a flat open-addressing table (linear probing, load <= 1/2).
+inline uint64_t hash_sv(sv s) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ s.size();
+  size_t i = 0;
+  for (; i + 8 <= s.size(); i += 8) {
+    uint64_t w;
+    memcpy(&w, s.data() + i, 8);
+    h = (h ^ w) * 0xFF51AFD7ED558CCDull;
+    h ^= h >> 32;
+  }
+  uint64_t w = 0;
+  memcpy(&w, s.data() + i, s.size() - i);
+  h = (h ^ w) * 0xC4CEB9FE1A85EC53ull;
+  return h ^ (h >> 29);
+}
+
+struct Pool {
+  std::vector<std::unique_ptr<char[]>> chunks;
+  size_t left = 0;
+  char* cur = nullptr;
+  std::vector<sv> strs;
+  std::vector<uint32_t> slots{std::vector<uint32_t>(64, 0)};  // id + 1, 0 = empty
+  std::vector<uint32_t> tags{std::vector<uint32_t>(64, 0)};   // hash bits for quick rejects
+
+  void reserve(size_t n) {
+    size_t cap = 64;
+    while (cap < 2 * n) cap <<= 1;
+    if (cap > slots.size()) rehash(cap);
+  }
+  sv store(sv s) {
+    if (s.size() > left) {
+      const size_t n = std::max<size_t>(s.size(), 1 << 20);
+      chunks.emplace_back(new char[n]);
+      cur = chunks.back().get();
+      left = n;
+    }
+    if (!s.empty()) memcpy(cur, s.data(), s.size());
+    sv out(cur, s.size());
+    cur += s.size();
+    left -= s.size();
+    return out;
+  }
+  void rehash(size_t cap) {
+    std::vector<uint32_t> ns(cap, 0), nt(cap, 0);
+    const size_t mask = cap - 1;
+    for (uint32_t id = 0; id < strs.size(); ++id) {
+      const uint64_t h = hash_sv(strs[id]);
+      size_t i = h & mask;
+      while (ns[i]) i = (i + 1) & mask;
+      ns[i] = id + 1;
+      nt[i] = (uint32_t)(h >> 32);
+    }
+    slots.swap(ns);
+    tags.swap(nt);
+  }
+  // slot of s (occupied when found, else the empty slot where it goes)
+  size_t probe(sv s, uint64_t h) const {
+    const size_t mask = slots.size() - 1;
+    size_t i = h & mask;
+    const uint32_t tg = (uint32_t)(h >> 32);
+    for (;;) {
+      const uint32_t v = slots[i];
+      if (!v || (tags[i] == tg && strs[v - 1] == s)) return i;
+      i = (i + 1) & mask;
+    }
+  }
+  int64_t find(sv s) const {
+    const uint32_t v = slots[probe(s, hash_sv(s))];
+    return v ? (int64_t)v - 1 : -1;
+  }
+  uint32_t intern(sv s) {
+    const uint64_t h = hash_sv(s);
+    size_t i = probe(s, h);
+    if (slots[i]) return slots[i] - 1;
+    const uint32_t id = (uint32_t)strs.size();
+    strs.push_back(store(s));
+    if (2 * strs.size() > slots.size()) {
+      rehash(slots.size() * 2);
+      return id;
+    }
+    slots[i] = id + 1;
+    tags[i] = (uint32_t)(h >> 32);
+    return id;
+  }
+};
+
 struct Model {
-  std::vector<std::string> ids;
-  std::unordered_map<std::string, uint32_t> id_index;
+  Pool ids, seqids, strands;
   std::vector<uint64_t> id_types;  // bitmask of tables holding the ID (<= 64 tables)
+  // feature stored under (table, ID): the ID's first table in `first_feat`,
+  // further tables (rare: the same ID under two types) in `more_feat`
+  std::vector<uint8_t> first_table;
+  std::vector<uint32_t> first_feat;
+  std::unordered_map<uint64_t, uint32_t> more_feat;
   std::vector<Table> tables;
   std::unordered_map<std::string, uint32_t> table_index;
   std::vector<uint32_t> rank;      // table -> rank in sorted-name order
-  std::vector<std::string> seqids, strands;
-  std::unordered_map<std::string, uint32_t> seqid_index, strand_index;
   std::vector<Feature> feats;
 
   Model() {
@@ -60,28 +154,35 @@ struct Model {
     for (const char* t : {"gene", "transcript", "CDS", "UTR"}) table(t);
   }
 
-  uint32_t intern(std::unordered_map<std::string, uint32_t>& idx, std::vector<std::string>& pool,
-                  const std::string& s) {
-    auto it = idx.find(s);
-    if (it != idx.end()) return it->second;
-    const uint32_t k = (uint32_t)pool.size();
-    pool.push_back(s);
-    idx.emplace(s, k);
+  uint32_t id(sv s) {
+    const uint32_t k = ids.intern(s);
+    while (id_types.size() < ids.strs.size()) {
+      id_types.push_back(0);
+      first_table.push_back(0);
+      first_feat.push_back(0);
+    }
     return k;
   }
-  uint32_t id(const std::string& s) {
-    const uint32_t k = intern(id_index, ids, s);
-    if (id_types.size() < ids.size()) id_types.resize(ids.size(), 0);
-    return k;
+  // feature of ID idk in table t (-1 when absent)
+  int64_t slot(uint32_t t, uint32_t idk) const {
+    if (!((id_types[idk] >> t) & 1)) return -1;
+    if (first_table[idk] == t) return first_feat[idk];
+    return more_feat.at(((uint64_t)idk << 6) | t);
   }
-  uint32_t table(const std::string& name) {
+  uint32_t table(sv name_sv) {
+    for (const Table& t : tables)  // few tables: a linear scan beats hashing
+      if (sv(t.name) == name_sv) return (uint32_t)(&t - tables.data());
+    return table_slow(name_sv);
+  }
+  uint32_t table_slow(sv name_sv) {
+    const std::string name(name_sv);
     auto it = table_index.find(name);
     if (it != table_index.end()) return it->second;
     // attributes of the instance that are not dicts (genome.py:524-545, plus
     // the object path's copy counter) cannot become feature tables
     if (name == "genome" || name == "_magot_copies" || tables.size() >= 64) throw Unsupported();
     const uint32_t k = (uint32_t)tables.size();
-    tables.push_back(Table{name, {}, {}});
+    tables.push_back(Table{name, {}});
     table_index.emplace(name, k);
     std::vector<uint32_t> order(tables.size());
     for (uint32_t i = 0; i < order.size(); ++i) order[i] = i;
@@ -95,23 +196,33 @@ struct Model {
   int64_t lookup(uint32_t idk) const {
     const uint64_t m = idk < id_types.size() ? id_types[idk] : 0;
     if (!m) return -1;
+    if (!(m & (m - 1))) return first_feat[idk];
     int best = -1;
     for (uint32_t t = 0; t < tables.size(); ++t)
       if ((m >> t) & 1)
         if (best < 0 || rank[t] > rank[(uint32_t)best]) best = (int)t;
-    return tables[(uint32_t)best].slot.at(idk);
+    return slot((uint32_t)best, idk);
+  }
+  int64_t lookup(sv s) const {
+    const int64_t k = ids.find(s);
+    return k < 0 ? -1 : lookup((uint32_t)k);
   }
   // table[ID] = feature (a dict assignment: an existing key keeps its position)
   void put(uint32_t t, uint32_t idk, uint32_t f) {
-    Table& tb = tables[t];
-    auto it = tb.slot.find(idk);
-    if (it == tb.slot.end()) {
-      tb.slot.emplace(idk, f);
-      tb.keys.push_back(idk);
-      id_types[idk] |= 1ull << t;
-    } else {
-      it->second = f;
+    const uint64_t m = id_types[idk];
+    if ((m >> t) & 1) {  // existing key: new value, same position
+      if (first_table[idk] == t) first_feat[idk] = f;
+      else more_feat[((uint64_t)idk << 6) | t] = f;
+      return;
     }
+    tables[t].keys.push_back(idk);
+    if (!m) {
+      first_table[idk] = (uint8_t)t;
+      first_feat[idk] = f;
+    } else {
+      more_feat[((uint64_t)idk << 6) | t] = f;
+    }
+    id_types[idk] = m | (1ull << t);
   }
 };
 
@@ -119,10 +230,12 @@ struct Model {
 // read_gff (genome.py:242-415) with the default arguments of gff2fasta
 // ---------------------------------------------------------------------------
 
-bool is_space(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
+inline bool is_space(char c) {
+  return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
+}
 
-std::vector<std::string> split_ws(const std::string& s) {  // str.split()
-  std::vector<std::string> out;
+void split_ws(sv s, std::vector<sv>& out) {  // str.split()
+  out.clear();
   size_t i = 0, n = s.size();
   while (i < n) {
     while (i < n && is_space(s[i])) ++i;
@@ -132,26 +245,11 @@ std::vector<std::string> split_ws(const std::string& s) {  // str.split()
     out.push_back(s.substr(i, j - i));
     i = j;
   }
-  return out;
-}
-
-std::vector<std::string> split_on(const std::string& s, char c) {  // str.split(c)
-  std::vector<std::string> out;
-  size_t i = 0;
-  for (;;) {
-    const size_t j = s.find(c, i);
-    if (j == std::string::npos) {
-      out.push_back(s.substr(i));
-      return out;
-    }
-    out.push_back(s.substr(i, j - i));
-    i = j + 1;
-  }
 }
 
 // int() of a coordinate column: optional surrounding whitespace and sign,
 // decimal digits.  Anything else (ValueError in the reference) -> object path.
-int64_t parse_int(const std::string& s) {
+int64_t parse_int(sv s) {
   size_t i = 0, n = s.size();
   while (i < n && is_space(s[i])) ++i;
   while (n > i && is_space(s[n - 1])) --n;
@@ -166,14 +264,14 @@ int64_t parse_int(const std::string& s) {
   return neg ? -v : v;
 }
 
-struct Tags {
-  std::vector<std::pair<std::string, std::string>> kv;
-  const std::string* get(const std::string& k) const {
-    for (auto it = kv.rbegin(); it != kv.rend(); ++it)
-      if (it->first == k) return &it->second;
+struct Tags {  // a dict: later assignments update the value in place
+  std::vector<std::pair<sv, sv>> kv;
+  const sv* get(sv k) const {
+    for (const auto& p : kv)
+      if (p.first == k) return &p.second;
     return nullptr;
   }
-  void set(const std::string& k, const std::string& v) {
+  void set(sv k, sv v) {
     for (auto& p : kv)
       if (p.first == k) {
         p.second = v;
@@ -184,12 +282,26 @@ struct Tags {
 };
 
 void read_gff(Model& M, const char* text, uint64_t n) {
+  {
+    // size the ID table from the line count (about one new ID per line)
+    uint64_t lines = 0;
+    for (const char* q = text; (q = static_cast<const char*>(memchr(q, '\n', text + n - q)));
+         ++q)
+      ++lines;
+    M.ids.reserve(lines / 2 + 16);
+    M.feats.reserve(lines / 2 + 16);
+  }
   int version = 0;  // 0 = auto
   bool have_id_field = true, have_parent_field = true;  // IDfield='ID', parent_field='Parent'
   std::vector<std::string> hierarchy;
   std::unordered_map<uint32_t, int64_t> renamed;
+  std::string scratch, idbuf;
+  std::vector<sv> words;
+  Tags tags;
+  sv last_seqid, last_strand;
+  uint32_t last_sq = 0, last_st = 0;
+  bool first_line = true;
   uint64_t pos = 0;
-  std::string line;
   while (pos < n) {
     const char* nl = static_cast<const char*>(memchr(text + pos, '\n', n - pos));
     const uint64_t end = nl ? (uint64_t)(nl - text) + 1 : n;
@@ -197,106 +309,160 @@ void read_gff(Model& M, const char* text, uint64_t n) {
     const uint64_t rl = end - pos;
     pos = end;
     if (raw[0] == '#') continue;
-    uint64_t tabs = 0;
-    for (uint64_t i = 0; i < rl; ++i) tabs += raw[i] == '\t';
+    // the 8 tabs (exactly) of an accepted line
+    uint32_t tpos[9];
+    int tabs = 0;
+    bool cr = false;
+    for (uint64_t i = 0; i < rl; ++i) {
+      const char ch = raw[i];
+      if (ch == '\t') {
+        if (tabs < 9) tpos[tabs] = (uint32_t)i;
+        ++tabs;
+      }
+      cr |= ch == '\r';
+    }
     if (tabs != 8) continue;
-    line.clear();
-    for (uint64_t i = 0; i < rl; ++i)
-      if (raw[i] != '\n' && raw[i] != '\r') line.push_back(raw[i]);
-    const std::vector<std::string> cols = split_on(line, '\t');
-    const std::string& tags_text = cols[8];
+    // line.replace('\n', '').replace('\r', '')  ('\n' only ends a line)
+    sv line(raw, rl);
+    if (cr) {
+      scratch.clear();
+      for (uint64_t i = 0; i < rl; ++i)
+        if (raw[i] != '\n' && raw[i] != '\r') scratch.push_back(raw[i]);
+      line = sv(scratch);
+      tabs = 0;
+      for (size_t i = 0; i < line.size(); ++i)
+        if (line[i] == '\t') tpos[tabs++] = (uint32_t)i;
+    } else if (rl && raw[rl - 1] == '\n') {
+      line = sv(raw, rl - 1);
+    }
+    sv cols[9];
+    {
+      size_t b = 0;
+      for (int c = 0; c < 8; ++c) {
+        cols[c] = line.substr(b, tpos[c] - b);
+        b = tpos[c] + 1;
+      }
+      cols[8] = line.substr(b);
+    }
+    const sv tags_text = cols[8];
     if (version == 0) {
-      if (tags_text.find('=') != std::string::npos) {
+      if (tags_text.find('=') != sv::npos) {
         version = 3;
       } else {
         version = 2;
-        std::string spaced = " " + tags_text;
+        std::string spaced = " " + std::string(tags_text);
         std::replace(spaced.begin(), spaced.end(), ';', ' ');
         if (have_id_field && hierarchy.empty() && spaced.find(" ID ") == std::string::npos) {
           have_id_field = false;
           have_parent_field = false;
-          const bool g = tags_text.find("gene_id") != std::string::npos;
-          const bool t = tags_text.find("transcript_id") != std::string::npos;
+          const bool g = tags_text.find("gene_id") != sv::npos;
+          const bool t = tags_text.find("transcript_id") != sv::npos;
           if (g && t) hierarchy = {"transcript_id", "gene_id"};
           else if (g) hierarchy = {"gene_id"};
         }
       }
     }
-    const std::string& seqid = cols[0];
-    const std::string& ftype = cols[2];
+    const sv seqid = cols[0];
+    const sv ftype = cols[2];
     if (ftype == "exon") continue;  // features_to_ignore default
     int64_t lo = parse_int(cols[3]), hi = parse_int(cols[4]);
     if (lo > hi) std::swap(lo, hi);
-    const std::string& strand = cols[6];
-    Tags tags;
-    for (const std::string& item : split_on(tags_text, ';')) {
-      if (item.empty()) continue;
-      if (version == 2) {
-        const std::vector<std::string> words = split_ws(item);
-        if (words.empty()) throw Unsupported();  // IndexError
-        const size_t q = item.find('"');
-        if (q != std::string::npos) {
-          const size_t q2 = item.find('"', q + 1);
-          tags.set(words[0], item.substr(q + 1, q2 == std::string::npos ? std::string::npos
-                                                                         : q2 - q - 1));
-        } else if (words.size() > 1) {
-          tags.set(words[0], words[1]);
-        } else {
-          throw Unsupported();  // print(item); return None
+    const sv strand = cols[6];
+    tags.kv.clear();
+    {
+      size_t b = 0;
+      for (;;) {
+        const size_t e = tags_text.find(';', b);
+        const sv item = tags_text.substr(b, e == sv::npos ? sv::npos : e - b);
+        if (!item.empty()) {
+          if (version == 2) {
+            split_ws(item, words);
+            if (words.empty()) throw Unsupported();  // IndexError
+            const size_t q = item.find('"');
+            if (q != sv::npos) {
+              const size_t q2 = item.find('"', q + 1);
+              tags.set(words[0], item.substr(q + 1, q2 == sv::npos ? sv::npos : q2 - q - 1));
+            } else if (words.size() > 1) {
+              tags.set(words[0], words[1]);
+            } else {
+              throw Unsupported();  // print(item); return None
+            }
+          } else {
+            const size_t q = item.find('=');
+            if (q == sv::npos) throw Unsupported();  // IndexError
+            const size_t q2 = item.find('=', q + 1);
+            tags.set(item.substr(0, q), item.substr(q + 1, q2 == sv::npos ? sv::npos : q2 - q - 1));
+          }
         }
-      } else {
-        const size_t e = item.find('=');
-        if (e == std::string::npos) throw Unsupported();  // IndexError
-        const size_t e2 = item.find('=', e + 1);
-        tags.set(item.substr(0, e),
-                 item.substr(e + 1, e2 == std::string::npos ? std::string::npos : e2 - e - 1));
+        if (e == sv::npos) break;
+        b = e + 1;
       }
     }
-    const std::string* parent = nullptr;
+    const sv* parent = nullptr;
     if (have_parent_field) {
       parent = tags.get("Parent");
     } else {
       for (const std::string& k : hierarchy)
         if ((parent = tags.get(k))) break;
     }
-    std::string ID;
-    if (have_id_field) {
-      if (const std::string* v = tags.get("ID")) ID = *v;
-      else if (parent) ID = *parent + "-" + ftype;
-      else throw Unsupported();  // ID None
+    sv ID;
+    if (have_id_field && tags.get("ID")) {
+      ID = *tags.get("ID");
+    } else if (have_id_field && !parent) {
+      throw Unsupported();  // ID None
     } else if (parent) {
-      ID = *parent + "-" + ftype;
+      idbuf.assign(parent->data(), parent->size());
+      idbuf += '-';
+      idbuf.append(ftype.data(), ftype.size());
+      ID = idbuf;
     } else {
-      ID = seqid + "-" + ftype + cols[3];
+      idbuf.assign(seqid.data(), seqid.size());
+      idbuf += '-';
+      idbuf.append(ftype.data(), ftype.size());
+      idbuf.append(cols[3].data(), cols[3].size());
+      ID = idbuf;
     }
     // de-duplicate against every table; the new name is not re-checked
+    uint32_t idk;
     {
-      const uint32_t k = M.id(ID);
-      if (M.lookup(k) >= 0) {
-        auto it = renamed.find(k);
+      const int64_t k0 = M.ids.find(ID);
+      if (k0 >= 0 && M.lookup((uint32_t)k0) >= 0) {
+        auto it = renamed.find((uint32_t)k0);
+        std::string nid(ID);
         if (it != renamed.end()) {
           it->second += 1;
-          ID = ID + "-" + std::to_string(it->second);
+          nid += "-" + std::to_string(it->second);
         } else {
-          renamed.emplace(k, 2);
-          ID = ID + "2";
+          renamed.emplace((uint32_t)k0, 2);
+          nid += "2";
         }
+        idk = M.id(nid);
+      } else {
+        idk = M.id(ID);
       }
     }
-    const uint32_t idk = M.id(ID);
-    const uint32_t sq = M.intern(M.seqid_index, M.seqids, seqid);
-    const uint32_t st = M.intern(M.strand_index, M.strands, strand);
+    // consecutive lines nearly always share seqid and strand
+    if (first_line || seqid != last_seqid) {
+      last_sq = M.seqids.intern(seqid);
+      last_seqid = M.seqids.strs[last_sq];
+    }
+    if (first_line || strand != last_strand) {
+      last_st = M.strands.intern(strand);
+      last_strand = M.strands.strs[last_st];
+    }
+    first_line = false;
+    const uint32_t sq = last_sq, st = last_st;
     if (parent) {
       uint32_t child = idk;
       for (size_t level = 0; level < hierarchy.size(); ++level) {
-        const std::string* pid = tags.get(hierarchy[level]);
+        const sv* pid = tags.get(hierarchy[level]);
         if (!pid) continue;
-        const std::string ptype = hierarchy[level].substr(0, hierarchy[level].find('_'));
-        const uint32_t t = M.table(ptype);
+        const std::string& hk = hierarchy[level];
+        const uint32_t t = M.table(sv(hk).substr(0, hk.find('_')));
         const uint32_t pk = M.id(*pid);
-        auto it = M.tables[t].slot.find(pk);
-        if (it != M.tables[t].slot.end()) {
-          auto& ch = M.feats[it->second].children;
+        const int64_t have = M.slot(t, pk);
+        if (have >= 0) {
+          auto& ch = M.feats[(size_t)have].children;
           if (std::find(ch.begin(), ch.end(), child) == ch.end()) ch.push_back(child);
         } else {
           Feature f;
@@ -310,7 +476,7 @@ void read_gff(Model& M, const char* text, uint64_t n) {
         }
         child = pk;
       }
-      const int64_t h = M.lookup(M.id(*parent));
+      const int64_t h = M.lookup(*parent);
       if (h < 0) throw Unsupported();                    // orphan: print, return None
       Feature& holder = M.feats[(size_t)h];
       if (holder.base) throw Unsupported();              // BaseAnnotation has no child_list
@@ -333,7 +499,7 @@ void read_gff(Model& M, const char* text, uint64_t n) {
 // CPython 2.7 dict order (magot_amd/py2order.py)
 // ---------------------------------------------------------------------------
 
-uint64_t py2_hash(const std::string& s) {
+uint64_t py2_hash(sv s) {
   if (s.empty()) return 0;
   uint64_t h = (uint64_t)(uint8_t)s[0] << 7;
   for (unsigned char c : s) h = (h * 1000003ull) ^ c;
@@ -450,15 +616,20 @@ struct Lowering {
         if (o < 0) throw Unsupported();
         const Feature& C = M.feats[(size_t)o];
         if (!C.base) throw Unsupported();  // mixed children: print
-        const std::string& sd = M.strands[C.strand];
+        const sv sd = M.strands.strs[C.strand];
         if (sd != "+" && sd != "." && sd != "-") throw Unsupported();  // invalid strand: print
-        auto ci = contig_of.find(M.seqids[C.seqid]);
-        if (ci == contig_of.end()) throw Unsupported();  // missing seqid: print
+        if (contig_idx.size() < M.seqids.strs.size()) contig_idx.resize(M.seqids.strs.size(), -2);
+        int64_t& cix = contig_idx[C.seqid];
+        if (cix == -2) {
+          auto ci = contig_of.find(std::string(M.seqids.strs[C.seqid]));
+          cix = ci == contig_of.end() ? -1 : (int64_t)ci->second;
+        }
+        if (cix < 0) throw Unsupported();  // missing seqid: print
         magot_exon x;
         uint64_t st, ln;
-        slice(C.lo - 1, C.hi, (int64_t)contig_len[ci->second], &st, &ln);
+        slice(C.lo - 1, C.hi, (int64_t)contig_len[cix], &st, &ln);
         x.start_rc = st | (sd == "-" ? kRcBit : 0);
-        x.contig = ci->second;
+        x.contig = (uint32_t)cix;
         x.len = (uint32_t)ln;
         if (ln >= 0xFFFFFFFFull) throw Unsupported();
         const std::pair<int64_t, int64_t> key(C.lo, C.hi);
@@ -474,12 +645,12 @@ struct Lowering {
       }
       std::stable_sort(by.begin(), by.end(),
                        [](const auto& a, const auto& b) { return a.first < b.first; });
-      if (M.strands[strand] == "-") std::reverse(by.begin(), by.end());
+      if (M.strands.strs[strand] == "-") std::reverse(by.begin(), by.end());
       uint64_t total = 0;
       for (auto& e : by) total += e.second.len;
       if (P.protein && total <= 2) throw Unsupported();  // translate() -> None
       if (!first_in_join) text("\n");
-      text(">" + M.ids[idk_of(fi)] + "\n");
+      text(">" + std::string(M.ids.strs[idk_of(fi)]) + "\n");
       magot_tx t;
       t.exon_begin = P.exons.size();
       t.n_exons = (uint32_t)by.size();
@@ -501,6 +672,7 @@ struct Lowering {
 
   // the ID a feature was stored under (ParentAnnotation.ID)
   std::vector<uint32_t> id_of_feat;
+  std::vector<int64_t> contig_idx;  // seqid -> contig (-1 missing, -2 unknown yet)
   uint32_t idk_of(uint32_t fi) const { return id_of_feat[fi]; }
 };
 
@@ -521,33 +693,46 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
   *out = nullptr;
   std::unique_ptr<magot_gffplan> P(new magot_gffplan());
   P->protein = (flags & MAGOT_GFF_PROTEIN) != 0;
+  const bool timing = std::getenv("MAGOT_GFF_TIMING") != nullptr;
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto t0 = now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    const auto t1 = now();
+    fprintf(stderr, "[gffplan] %-10s %.3f s\n", what,
+            std::chrono::duration<double>(t1 - t0).count());
+    t0 = t1;
+  };
   try {
     magot::read_gff(P->model, gff, gff_len);
+    lap("read_gff");
     magot::Model& M = P->model;
     std::unordered_map<std::string, uint32_t> contig_of;
     for (uint32_t i = 0; i < n_contigs; ++i) contig_of[seqids[i]] = i;  // last duplicate wins
-    magot::Lowering L{*P, contig_of, contig_lens, {}};
+    magot::Lowering L{*P, contig_of, contig_lens, {}, {}};
     L.id_of_feat.assign(M.feats.size(), 0);
-    for (const magot::Table& t : M.tables)
-      for (uint32_t k : t.keys) L.id_of_feat[t.slot.at(k)] = k;
+    for (uint32_t ti2 = 0; ti2 < M.tables.size(); ++ti2)
+      for (uint32_t k : M.tables[ti2].keys) L.id_of_feat[(size_t)M.slot(ti2, k)] = k;
     auto ti = M.table_index.find(feature);
     if (ti == M.table_index.end()) throw Unsupported();  // AttributeError
     const magot::Table& T = M.tables[ti->second];
     std::vector<uint32_t> keys = T.keys;
     if (flags & MAGOT_GFF_ORDER_PY2) {
-      std::vector<uint64_t> hash(M.ids.size());
-      for (uint32_t k : keys) hash[k] = magot::py2_hash(M.ids[k]);
+      std::vector<uint64_t> hash(M.ids.strs.size());
+      for (uint32_t k : keys) hash[k] = magot::py2_hash(M.ids.strs[k]);
       keys = magot::py2_dict_order(keys, hash);  // the table as built ...
       keys = magot::py2_dict_order(keys, hash);  // ... and as deep-copied (genome.py:415)
     }
+    lap("order");
     // "\n".join(obj.get_fasta() for obj in table.values()): every object adds
     // its records (a blank line when it has none)
     for (size_t i = 0; i < keys.size(); ++i) {
-      const uint32_t fi = T.slot.at(keys[i]);
+      const uint32_t fi = (uint32_t)M.slot(ti->second, keys[i]);
       if (M.feats[fi].base) throw Unsupported();  // BaseAnnotation has no get_fasta
       if (i) L.text("\n");
       L.fasta(fi, true);
     }
+    lap("lower");
   } catch (const Unsupported&) {
     magot::set_error("magot_gff_plan: input takes a diagnostic path; use the object path");
     return MAGOT_ERR_UNSUPPORTED;

@@ -1,0 +1,106 @@
+"""End-to-end gff2fasta on a BASELINE-shaped synthetic (default C3): writes the
+FASTA + GFF3 text files, then times each phase of the native CLI path
+(genome_tools._gff2fasta_native) -- FASTA parse, native GFF plan, genome pack
++ H2D, plan upload, kernel, D2H, text render -- and checks the output
+against the C oracle's record bytes.  Writes one JSON line.
+
+    python scripts/e2e_cli.py [--config C3] [--seq-type protein] [--dir /tmp/magot_e2e]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from magot_amd import engine, genome, synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--config', default='C3')
+    ap.add_argument('--seq-type', default='protein')
+    ap.add_argument('--dir', default='/tmp/magot_e2e')
+    ap.add_argument('--order', default='py2')
+    a = ap.parse_args()
+    os.makedirs(a.dir, exist_ok=True)
+    fa, gf = os.path.join(a.dir, 'genome.fa'), os.path.join(a.dir, 'ann.gff3')
+    t = time.perf_counter()
+    w = synth.make(a.config)
+    with open(fa, 'w') as fh:
+        fh.write(w.fasta_text())
+    with open(gf, 'w') as fh:
+        fh.write(w.gff3_text())
+    t_gen = time.perf_counter() - t
+    ph = {}
+    t0 = time.perf_counter()
+    seqs = genome.GenomeSequence(fa)
+    ph['fasta_parse'] = time.perf_counter() - t0
+    t = time.perf_counter()
+    names = list(seqs)
+    protein = a.seq_type == 'protein'
+    plan = engine.GffPlan.build(genome.ensure_file(gf).read(), names,
+                                [len(seqs[n]) for n in names], protein=protein, order=a.order)
+    ph['gff_read_and_plan_native'] = time.perf_counter() - t
+    assert plan is not None
+    t = time.perf_counter()
+    dev = seqs.device()
+    ph['genome_pack_h2d'] = time.perf_counter() - t
+    t = time.perf_counter()
+    ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
+                               engine.OUT_PEP if protein else engine.OUT_NUC)
+    ph['plan_h2d'] = time.perf_counter() - t
+    t = time.perf_counter()
+    ex.execute()
+    ex.sync()
+    ph['kernel'] = time.perf_counter() - t
+    t = time.perf_counter()
+    nuc, noff, pep, poff = ex.fetch()
+    ph['d2h'] = time.perf_counter() - t
+    t = time.perf_counter()
+    text = plan.render(nuc, noff, pep, poff)
+    ph['render'] = time.perf_counter() - t
+    t = time.perf_counter()
+    with open(os.path.join(a.dir, 'out.fa'), 'wb') as fh:
+        fh.write(text)
+        fh.write(b'\n')
+    ph['write'] = time.perf_counter() - t
+    total = time.perf_counter() - t0
+    kernel_ms = ex.time(10)
+    # payload check against the C oracle on the same tables
+    from oracle import cds_oracle
+    ex_t, tx_t = plan.exons, plan.txs
+    st = ex_t['start_rc'].astype(np.uint64)
+    rc = (st >> np.uint64(63)).astype(bool)
+    start = (st & np.uint64((1 << 63) - 1)).astype(np.int64)
+    rec_off = np.zeros(len(tx_t) + 1, dtype=np.int64)
+    np.cumsum(tx_t['n_exons'].astype(np.int64), out=rec_off[1:])
+    ref, roff, rst = cds_oracle.extract(w.genome, w.contig_off, rec_off, ex_t['contig'],
+                                        start + 1, start + ex_t['len'].astype(np.int64),
+                                        np.where(rc, ord('-'), ord('+')).astype(np.uint8),
+                                        protein)
+    if not protein:
+        ok = bool(np.array_equal(nuc, ref) and np.array_equal(noff.astype(np.int64), roff))
+    else:
+        starts = poff[:-1].astype(np.int64)
+        lens = (poff[1:] - poff[:-1]).astype(np.int64)
+        first = np.zeros(len(starts), dtype=bool)
+        first[lens > 0] = pep[starts[lens > 0]] == ord('X')
+        keep = np.ones(len(pep), dtype=bool)
+        keep[starts[first]] = False
+        ok = bool(np.array_equal(pep[keep], ref))
+    rec = {'config': a.config, 'seq_type': a.seq_type, 'order': a.order,
+           'records': int(len(plan.txs)), 'intervals': int(len(plan.exons)),
+           'cds_bases': int(w.cds_bases), 'output_bytes': len(text) + 1,
+           'gff_lines': None, 'phases_s': ph, 'end_to_end_s': total,
+           'kernel_ms_hip_events': kernel_ms, 'generate_files_s': t_gen,
+           'payload_check': ok}
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == '__main__':
+    main()

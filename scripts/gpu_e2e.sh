@@ -1,0 +1,9 @@
+#!/bin/bash
+# End-to-end CLI path on C3 (native planner + one kernel launch).
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/e2e; mkdir -p $OUT
+timeout -k 10 900 python scripts/e2e_cli.py --config C3 --seq-type protein > $OUT/e2e_protein.json 2> $OUT/e2e.err || { tail -20 $OUT/e2e.err; exit 1; }
+cat $OUT/e2e_protein.json
+rm -rf /tmp/magot_e2e
