@@ -93,6 +93,19 @@ def _read_source(potential_file):
     return data
 
 
+def read_bytes(potential_file):
+    """ensure_file's content as raw bytes (latin-1 for text), for native parsers."""
+    if hasattr(potential_file, 'read'):
+        data = potential_file.read()
+    else:
+        try:
+            with open(potential_file, 'rb') as fh:
+                return fh.read()
+        except (OSError, ValueError):
+            data = potential_file
+    return data if isinstance(data, (bytes, bytearray)) else data.encode('latin-1')
+
+
 def ensure_file(potential_file):
     """magot_smallfuncs.py:32-43: a path is opened; a string that cannot be
     opened is itself the content; a file object passes through."""

@@ -71,7 +71,7 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order):
     seqs = genome.GenomeSequence(genome_sequence)
     names = list(seqs)
     protein = seq_type == 'protein'
-    plan = engine.GffPlan.build(genome.ensure_file(gff).read(), names,
+    plan = engine.GffPlan.build(genome.read_bytes(gff), names,
                                 [len(seqs[n]) for n in names], protein=protein, order=order)
     if plan is None:
         return None

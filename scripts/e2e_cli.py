@@ -43,7 +43,7 @@ def main():
     t = time.perf_counter()
     names = list(seqs)
     protein = a.seq_type == 'protein'
-    plan = engine.GffPlan.build(genome.ensure_file(gf).read(), names,
+    plan = engine.GffPlan.build(genome.read_bytes(gf), names,
                                 [len(seqs[n]) for n in names], protein=protein, order=a.order)
     ph['gff_read_and_plan_native'] = time.perf_counter() - t
     assert plan is not None
