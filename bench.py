@@ -47,8 +47,10 @@ def dist_setup(n_gpus):
     import torch.distributed as dist
     backend = 'gloo'
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
+        # one GPU per rank; MAGOT_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
+        torch.cuda.set_device(local % torch.cuda.device_count())
         backend = 'nccl'            # RCCL on ROCm
+    backend = os.environ.get('MAGOT_DIST_BACKEND', backend)
     dist.init_process_group(backend=backend)
     return dist, rank, local, world
 
@@ -139,6 +141,119 @@ def cpu_baseline(w, budget_bases):
                                                    t2 - t1)}
 
 
+def strong_main(args, dist, rank, local, world):
+    """C4: the single C3 job on `world` GPUs.
+
+    A step = every rank extracts its contig shard + its outputs are gathered
+    to rank 0 over the collective backend (RCCL/xGMI with nccl).  Reported:
+    `value` (bases/s with the gather), the extraction-only rate, and the
+    one-off genome broadcast time."""
+    import torch
+
+    from magot_amd import _lib, engine, shard, synth
+    if dist is None:
+        import torch.distributed as tdist
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29517')
+        torch.cuda.set_device(local)
+        tdist.init_process_group('nccl', rank=0, world_size=1)
+        dist = tdist
+    t0 = time.perf_counter()
+    w = synth.make(args.config, seed=shard_seed(args.config, 0))  # the same job on every rank
+    t_gen = time.perf_counter() - t0
+    ctx = _lib.Context(local)
+    tx_bases = np.bincount(np.repeat(np.arange(w.n_tx), w.ex_count), weights=w.ex_len,
+                           minlength=w.n_tx)
+    owner, shards, load = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), world)
+    mine = shards[rank]
+    log('C4: %d records over %d ranks, LPT load imbalance %.2f%%'
+        % (w.n_tx, world, 100.0 * (load.max() / max(load.mean(), 1.0) - 1.0)))
+    dev, t_bcast = shard.replicate_genome(dist, rank, w.contigs() if rank == 0 else None, ctx)
+    t_bcast = allreduce_max(dist, t_bcast)
+    ex, tx = w.plan_tables(tx_subset=mine)
+    outputs = engine.OUT_NUC | (engine.OUT_PEP if w.outputs == 'nuc+pep' else 0)
+    plan = engine.ExtractionPlan(dev, ex, tx, outputs)
+    B, P = plan.nuc_bytes, plan.pep_bytes
+    # output gathers: send buffers sized for the largest rank, filled D2D by
+    # magot_plan_copy_outputs, gathered to rank 0 device memory every step
+    gn = shard.Gather(dist, rank, world, B)
+    gp = shard.Gather(dist, rank, world, P) if outputs & engine.OUT_PEP else None
+
+    def step():
+        plan.execute()
+        plan.copy_outputs(gn.send.data_ptr(), gp.send.data_ptr() if gp is not None and P else None)
+        gn.run()
+        if gp is not None:
+            gp.run()
+
+    # correctness: rank 0 reassembles the global outputs and checks them
+    parity = 'not checked'
+    step()
+    g_nuc = gn.parts()
+    g_pep = gp.parts() if gp is not None else None
+    _, noff, _, poff = plan.fetch()
+    offs = [None] * world
+    dist.gather_object((noff.tolist(), poff.tolist()), offs if rank == 0 else None, dst=0)
+    if rank == 0 and not args.no_verify:
+        from oracle import cds_oracle
+        nuc, goff = shard.reassemble(shards, g_nuc, [o[0] for o in offs])
+        ref, roff, st = cds_oracle.extract_workload(w, False)
+        ok = (not st.any()) and np.array_equal(nuc, ref) and np.array_equal(goff, roff)
+        if ok and g_pep is not None:
+            pep, pgoff = shard.reassemble(shards, g_pep, [o[1] for o in offs])
+            pref, proff, pst = cds_oracle.extract_workload(w, True)
+            starts, lens = pgoff[:-1], pgoff[1:] - pgoff[:-1]
+            first = np.zeros(len(starts), dtype=bool)
+            first[lens > 0] = pep[starts[lens > 0]] == ord('X')
+            keep = np.ones(len(pep), dtype=bool)
+            keep[starts[first]] = False
+            ok = np.array_equal(pep[keep], pref)
+        parity = 'bit-exact vs CPU oracle (gathered, global record order)' if ok else 'MISMATCH'
+    del g_nuc, g_pep
+
+    def timed(fn, k):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        barrier(dist)
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t
+        barrier(dist)
+        return allreduce_max(dist, el)
+
+    el_full = timed(step, args.steps)
+    el_kernel = timed(lambda: (plan.execute(), ctx.sync()), args.steps)
+    total = allreduce_sum(dist, float(B))
+    if rank == 0:
+        rec = {
+            'metric': 'CDS bases extracted+translated/sec',
+            'value': total * args.steps / el_full,
+            'unit': 'bases/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': el_full / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'strong', 'vs_baseline': None, 'dtype': 'u8',
+            'data': 'synthetic (seeded, SURVEY.md 8(d))',
+            'config': {'workload': 'C4: one %s job (1 Gb genome, 500k transcripts) over %d GPUs; '
+                                   'genome packed on rank 0 and broadcast, records sharded by '
+                                   'contig (LPT), outputs gathered to rank 0 every step'
+                                   % (args.config, world),
+                       'cds_bases': int(total), 'parallelism': 'contig-sharded x%d (strong)' % world,
+                       'backend': dist.get_backend()},
+            'extract_only': {'value': total * args.steps / el_kernel,
+                             'ms_per_step': el_kernel / args.steps * 1e3},
+            'genome_broadcast_s': t_bcast,
+            'lpt_imbalance': float(load.max() / max(load.mean(), 1.0) - 1.0),
+            'parity': parity,
+            'phases_s': {'generate': t_gen},
+        }
+        print(json.dumps(rec), flush=True)
+    plan.close()
+    dev.close()
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -150,10 +265,19 @@ def main():
     ap.add_argument('--cpu-sample-bases', type=float, default=5.0e7)
     ap.add_argument('--pmc-json', default=os.path.join(ROOT, 'profiles', 'pmc_C3.json'),
                     help='per-launch HBM traffic measured with rocprofv3 --pmc')
+    ap.add_argument('--mode', default='weak', choices=['weak', 'strong'],
+                    help='weak: one C3-shaped shard per rank (default); strong: BASELINE '
+                         'configs[3] (C4) -- one C3 job, genome packed once and broadcast, '
+                         'records sharded by contig, outputs gathered to rank 0')
     args = ap.parse_args()
 
     dist, rank, local, world = dist_setup(args.gpus)
+    if os.environ.get('MAGOT_DIST_BACKEND') == 'gloo':
+        import torch
+        local = local % max(torch.cuda.device_count(), 1)
     os.environ.setdefault('MAGOT_DEVICE', str(local))
+    if args.mode == 'strong':
+        return strong_main(args, dist, rank, local, world)
 
     from magot_amd import _lib, engine, synth
 

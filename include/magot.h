@@ -111,6 +111,22 @@ int magot_genome_stats(const magot_genome* g, uint64_t* total_bases, uint64_t* n
 void magot_genome_destroy(magot_genome* g);
 
 /*
+ * Genome replication across ranks (one packed genome broadcast
+ * over RCCL/xGMI instead of every rank packing its own).  The packed genome
+ * is one device arena plus a host meta blob:
+ *   magot_genome_export    meta blob (meta == NULL: size only) and arena size;
+ *   magot_genome_copy_arena D2D copy of the arena into caller device memory
+ *                          (e.g. the tensor a collective broadcasts);
+ *   magot_genome_attach    a genome over caller device memory holding a
+ *                          broadcast arena (not freed by magot_genome_destroy).
+ */
+int magot_genome_export(const magot_genome* g, uint8_t* meta, uint64_t cap, uint64_t* meta_len,
+                        uint64_t* arena_bytes);
+int magot_genome_copy_arena(const magot_genome* g, void* dst_dev);
+int magot_genome_attach(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len, void* arena_dev,
+                        magot_genome** out);
+
+/*
  * Build a device-resident plan: interval table -> output offsets, ~3 KiB
  * wave tiles, per-tile exon and record ranges, all uploaded to HBM.
  * nuc_bytes / pep_bytes receive the total output sizes (pep_bytes counts the
@@ -143,6 +159,10 @@ int magot_run(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off
  * HIP events around each launch; *avg_ms receives the mean launch duration.
  */
 int magot_plan_time(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms);
+
+/* D2D copy of a plan's outputs (nuc_bytes / pep_bytes) into caller device
+ * memory, e.g. the buffers an output gather sends. */
+int magot_plan_copy_outputs(magot_ctx* ctx, magot_plan* p, void* nuc_dst_dev, void* pep_dst_dev);
 
 /* Device-resident output pointers of a plan (for on-device consumers/tests). */
 int magot_plan_device_outputs(magot_plan* p, void** nuc_dev, void** pep_dev);

@@ -31,6 +31,8 @@ EXPORTS = (
     'magot_plan_algorithmic_bytes',
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
     'magot_gff_plan', 'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
+    'magot_genome_export', 'magot_genome_copy_arena', 'magot_genome_attach',
+    'magot_plan_copy_outputs',
 )
 
 ERR_UNSUPPORTED = -5
@@ -87,6 +89,11 @@ def _declare(lib):
         'magot_gffplan_render': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
                                                 _u64p]),
         'magot_gffplan_destroy': (None, [_vp]),
+        'magot_genome_export': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _u64p, _u64p]),
+        'magot_genome_copy_arena': (ctypes.c_int, [_vp, _vp]),
+        'magot_genome_attach': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp,
+                                               ctypes.POINTER(_vp)]),
+        'magot_plan_copy_outputs': (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

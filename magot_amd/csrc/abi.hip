@@ -44,6 +44,7 @@ struct magot_genome {
   magot_ctx* ctx = nullptr;
   void* arena = nullptr;
   uint64_t arena_bytes = 0;
+  bool owns_arena = true;  // false: caller memory (magot_genome_attach)
   uint32_t* nib = nullptr;  // forward then reverse-strand nibble plane (ExtractArgs::span)
   uint64_t span = 0;
   ExcRun* runs = nullptr;
@@ -85,6 +86,67 @@ int bind(magot_ctx* ctx) {
   }
   MAGOT_HIP_TRY(hipSetDevice(ctx->device));
   return MAGOT_OK;
+}
+
+}  // namespace
+
+// Host meta blob of a packed genome (magot_genome_export / _attach).
+namespace {
+
+struct MetaWriter {
+  std::vector<uint8_t> buf;
+  template <class T>
+  void put(const T& v) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+    buf.insert(buf.end(), p, p + sizeof(T));
+  }
+  template <class T>
+  void put_vec(const std::vector<T>& v) {
+    put<uint64_t>(v.size());
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(v.data());
+    buf.insert(buf.end(), p, p + v.size() * sizeof(T));
+  }
+};
+
+struct MetaReader {
+  const uint8_t* p;
+  const uint8_t* end;
+  template <class T>
+  bool get(T* v) {
+    if ((uint64_t)(end - p) < sizeof(T)) return false;
+    memcpy(v, p, sizeof(T));
+    p += sizeof(T);
+    return true;
+  }
+  template <class T>
+  bool get_vec(std::vector<T>* v) {
+    uint64_t n;
+    if (!get(&n) || n > (uint64_t)(end - p) / sizeof(T)) return false;
+    v->resize(n);
+    memcpy(v->data(), p, n * sizeof(T));
+    p += n * sizeof(T);
+    return true;
+  }
+};
+
+constexpr uint64_t kMetaMagic = 0x4d41474f54474e31ull;  // "MAGOTGN1"
+
+std::vector<uint8_t> genome_meta(const magot_genome* g) {
+  MetaWriter w;
+  w.put(kMetaMagic);
+  w.put(g->arena_bytes);
+  w.put<uint64_t>((const char*)g->nib - (const char*)g->arena);
+  w.put<uint64_t>((const char*)g->runs - (const char*)g->arena);
+  w.put<uint64_t>((const char*)g->dir - (const char*)g->arena);
+  w.put(g->span);
+  w.put(g->extent);
+  w.put(g->total_bases);
+  w.put(g->n_runs);
+  w.put_vec(g->contig_base);
+  w.put_vec(g->contig_len);
+  w.put_vec(g->host_runs);
+  w.put_vec(g->host_dir);
+  return w.buf;
 }
 
 }  // namespace
@@ -213,8 +275,70 @@ int magot_genome_stats(const magot_genome* g, uint64_t* total_bases, uint64_t* n
 void magot_genome_destroy(magot_genome* g) {
   if (!g) return;
   if (g->ctx) (void)hipSetDevice(g->ctx->device);
-  if (g->arena) (void)hipFree(g->arena);
+  if (g->arena && g->owns_arena) (void)hipFree(g->arena);
   delete g;
+}
+
+// --- replication (one packed genome broadcast to every rank) ---------------
+
+int magot_genome_export(const magot_genome* g, uint8_t* meta, uint64_t cap, uint64_t* meta_len,
+                        uint64_t* arena_bytes) {
+  if (!g || !meta_len) {
+    set_error("magot_genome_export: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  const std::vector<uint8_t> m = genome_meta(g);
+  *meta_len = m.size();
+  if (arena_bytes) *arena_bytes = g->arena_bytes;
+  if (!meta) return MAGOT_OK;
+  if (cap < m.size()) {
+    set_error("magot_genome_export: meta buffer too small");
+    return MAGOT_ERR_ARG;
+  }
+  memcpy(meta, m.data(), m.size());
+  return MAGOT_OK;
+}
+
+int magot_genome_copy_arena(const magot_genome* g, void* dst_dev) {
+  if (!g || !dst_dev) {
+    set_error("magot_genome_copy_arena: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (int rc = bind(g->ctx)) return rc;
+  MAGOT_HIP_TRY(hipMemcpyAsync(dst_dev, g->arena, g->arena_bytes, hipMemcpyDeviceToDevice,
+                               g->ctx->stream));
+  MAGOT_HIP_TRY(hipStreamSynchronize(g->ctx->stream));
+  return MAGOT_OK;
+}
+
+int magot_genome_attach(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len, void* arena_dev,
+                        magot_genome** out) {
+  if (int rc = bind(ctx)) return rc;
+  if (!meta || !arena_dev || !out) {
+    set_error("magot_genome_attach: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  std::unique_ptr<magot_genome> g(new magot_genome());
+  MetaReader r{meta, meta + meta_len};
+  uint64_t magic = 0, o_nib = 0, o_runs = 0, o_dir = 0;
+  bool ok = r.get(&magic) && magic == kMetaMagic && r.get(&g->arena_bytes) && r.get(&o_nib) &&
+            r.get(&o_runs) && r.get(&o_dir) && r.get(&g->span) && r.get(&g->extent) &&
+            r.get(&g->total_bases) && r.get(&g->n_runs) && r.get_vec(&g->contig_base) &&
+            r.get_vec(&g->contig_len) && r.get_vec(&g->host_runs) && r.get_vec(&g->host_dir);
+  if (!ok || o_nib >= g->arena_bytes || o_runs >= g->arena_bytes || o_dir >= g->arena_bytes) {
+    set_error("magot_genome_attach: malformed genome meta");
+    return MAGOT_ERR_ARG;
+  }
+  g->ctx = ctx;
+  g->arena = arena_dev;
+  g->owns_arena = false;
+  char* base = static_cast<char*>(arena_dev);
+  g->nib = reinterpret_cast<uint32_t*>(base + o_nib);
+  g->runs = reinterpret_cast<ExcRun*>(base + o_runs);
+  g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
+  *out = g.release();
+  return MAGOT_OK;
 }
 
 int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* exons,
@@ -519,6 +643,22 @@ int magot_plan_time(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms) {
   }
   p->executed = true;
   *avg_ms = total / iters;
+  return MAGOT_OK;
+}
+
+int magot_plan_copy_outputs(magot_ctx* ctx, magot_plan* p, void* nuc_dst_dev, void* pep_dst_dev) {
+  if (int rc = bind(ctx)) return rc;
+  if (!p) {
+    set_error("magot_plan_copy_outputs: null plan");
+    return MAGOT_ERR_ARG;
+  }
+  if (nuc_dst_dev && p->args.total_nuc && (p->args.outputs & MAGOT_OUT_NUC))
+    MAGOT_HIP_TRY(hipMemcpyAsync(nuc_dst_dev, p->args.nuc, p->args.total_nuc,
+                                 hipMemcpyDeviceToDevice, ctx->stream));
+  if (pep_dst_dev && p->args.total_pep && (p->args.outputs & MAGOT_OUT_PEP))
+    MAGOT_HIP_TRY(hipMemcpyAsync(pep_dst_dev, p->args.pep, p->args.total_pep,
+                                 hipMemcpyDeviceToDevice, ctx->stream));
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   return MAGOT_OK;
 }
 

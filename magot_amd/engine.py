@@ -44,17 +44,58 @@ class DeviceGenome(object):
         check(L.magot_genome_load(self.ctx.handle, ptrs, lens.ctypes.data_as(_lib._u64p), n,
                                   ctypes.byref(h)), 'magot_genome_load')
         self.handle = h
+        self._keepalive = None
+        self._stats()
+
+    def _stats(self):
         tb, nr, db = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-        check(L.magot_genome_stats(h, ctypes.byref(tb), ctypes.byref(nr), ctypes.byref(db)),
-              'magot_genome_stats')
+        check(_lib.lib().magot_genome_stats(self.handle, ctypes.byref(tb), ctypes.byref(nr),
+                                            ctypes.byref(db)), 'magot_genome_stats')
         self.total_bases = tb.value
         self.n_exception_runs = nr.value
         self.device_bytes = db.value
+
+    # -- replication (magot_genome_export / copy_arena / attach) -------------
+    def export(self):
+        """(meta bytes, arena size in bytes) of the packed genome."""
+        L = _lib.lib()
+        n, ab = ctypes.c_uint64(), ctypes.c_uint64()
+        check(L.magot_genome_export(self.handle, None, 0, ctypes.byref(n), ctypes.byref(ab)),
+              'magot_genome_export')
+        meta = np.empty(n.value, dtype=np.uint8)
+        check(L.magot_genome_export(self.handle, ptr(meta), n.value, ctypes.byref(n),
+                                    ctypes.byref(ab)), 'magot_genome_export')
+        return meta.tobytes(), ab.value
+
+    def copy_arena(self, dst_dev_ptr):
+        """D2D copy of the packed arena to caller device memory (an address)."""
+        check(_lib.lib().magot_genome_copy_arena(self.handle, ctypes.c_void_p(dst_dev_ptr)),
+              'magot_genome_copy_arena')
+
+    @classmethod
+    def attach(cls, meta, arena_dev_ptr, names, lengths, ctx=None, keepalive=None):
+        """A genome over caller device memory that holds a broadcast arena.
+        ``keepalive`` (e.g. the tensor owning the memory) lives as long as this."""
+        self = cls.__new__(cls)
+        self.ctx = ctx or _lib.default_context()
+        self.names = list(names)
+        self.index = {nm: i for i, nm in enumerate(self.names)}
+        self.lengths = np.asarray(lengths, dtype=np.uint64)
+        self._keepalive = keepalive
+        m = np.frombuffer(meta, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        check(_lib.lib().magot_genome_attach(self.ctx.handle, ptr(m), len(m),
+                                             ctypes.c_void_p(arena_dev_ptr), ctypes.byref(h)),
+              'magot_genome_attach')
+        self.handle = h
+        self._stats()
+        return self
 
     def close(self):
         if getattr(self, 'handle', None):
             _lib.lib().magot_genome_destroy(self.handle)
             self.handle = None
+        self._keepalive = None
 
     def __del__(self):
         try:
@@ -111,6 +152,13 @@ class ExtractionPlan(object):
     def run(self):
         self.execute()
         return self.fetch()
+
+    def copy_outputs(self, nuc_dev_ptr=None, pep_dev_ptr=None):
+        """D2D copy of the outputs into caller device memory (addresses)."""
+        check(_lib.lib().magot_plan_copy_outputs(
+            self.ctx.handle, self.handle,
+            ctypes.c_void_p(nuc_dev_ptr) if nuc_dev_ptr else None,
+            ctypes.c_void_p(pep_dev_ptr) if pep_dev_ptr else None), 'magot_plan_copy_outputs')
 
     def time(self, iters):
         ms = ctypes.c_double()
