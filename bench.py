@@ -254,6 +254,92 @@ def strong_main(args, dist, rank, local, world):
     dist.destroy_process_group()
 
 
+def orf6_main(args, dist, rank, local, world):
+    """C5 (BASELINE configs[4]): 3 Gb genome, 2M transcripts; a step gathers
+    every transcript's CDS (extract_kernel, nucleotide output kept in HBM) and
+    produces its six translations (orf6_kernel, Sequence.get_orfs's
+    frame x strand loop).  Weak scaling per rank like the default mode."""
+    from magot_amd import _lib, engine, synth
+    t0 = time.perf_counter()
+    w = synth.make(args.config, seed=shard_seed(args.config, rank))
+    t_gen = time.perf_counter() - t0
+    ctx = _lib.Context(local)
+    dev = engine.DeviceGenome(w.contigs(), ctx=ctx)
+    ex, tx = w.plan_tables()
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    o6 = engine.Orf6Plan(plan)
+    B = plan.nuc_bytes
+    R = None  # real six-frame residues (the padded buffer is o6.total)
+    parity = 'not checked'
+    if not args.no_verify:
+        from oracle import cds_oracle
+        from oracle import magot_oracle as mo
+        plan.execute()
+        o6.execute()
+        nuc, noff, _, _ = plan.fetch()
+        out, soff, slen = o6.fetch()
+        ref, roff, st = cds_oracle.extract_workload(w, False)
+        ok = (not st.any()) and np.array_equal(nuc, ref)
+        rng = np.random.default_rng(rank)
+        for r in rng.choice(len(tx), size=min(2000, len(tx)), replace=False):
+            sq = nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1')
+            for k, (f, strand) in enumerate((f, s2) for f in (0, 1, 2) for s2 in ('-', '+')):
+                j6 = 6 * r + k
+                t = out[int(soff[j6]):int(soff[j6] + slen[j6])].tobytes().decode('latin-1')
+                if k < 2 and t[:1] == 'X':
+                    t = t[1:]
+                want = mo.translate(sq, frame=f, strand=strand)
+                ok = ok and (t == (want or ''))
+        parity = ('bit-exact vs CPU oracle (nucleotide: full; six frames: 2000 sampled '
+                  'records)') if ok else 'MISMATCH'
+        del nuc, out
+    _, _, slen = o6.fetch()
+    R = int(slen.sum())
+    for _ in range(args.warmup):
+        plan.execute()
+        o6.execute()
+    ctx.sync()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan.execute()
+        o6.execute()
+    ctx.sync()
+    elapsed = time.perf_counter() - t0
+    barrier(dist)
+    elapsed_max = allreduce_max(dist, elapsed)
+    k_ex = plan.time(10)
+    k_o6 = o6.time(10)
+    total_bases = allreduce_sum(dist, float(B))
+    # algorithmic bytes (SURVEY 8(d), C5): 2-bit genome reads + six translations + descriptors
+    alg = -(-B // 4) + R + 16 * int(plan.n_exons) + 32 * int(plan.n_tx)
+    achieved = alg / ((k_ex + k_o6) * 1e-3) / 1e9
+    if rank == 0:
+        rec = {
+            'metric': 'CDS bases extracted+translated/sec', 'value': total_bases * args.steps /
+            elapsed_max, 'unit': 'bases/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': elapsed_max / args.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8',
+            'data': 'synthetic (seeded, SURVEY.md 8(d))',
+            'config': {'workload': 'C5 per rank: 3 Gb genome (200 contigs), 2M transcripts; '
+                                   'CDS gather + six-frame translation (get_orfs)',
+                       'cds_bases_per_rank': B, 'six_frame_residues_per_rank': R,
+                       'parallelism': 'contig-sharded x%d (weak)' % world},
+            'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                         'kernel': 'extract_kernel + orf6_kernel',
+                         'kernel_ms': {'extract': k_ex, 'orf6': k_o6},
+                         'algorithmic_bytes_per_step': alg},
+            'cpu_baseline': None, 'parity': parity, 'phases_s': {'generate': t_gen},
+        }
+        print(json.dumps(rec), flush=True)
+    o6.close()
+    plan.close()
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -278,6 +364,8 @@ def main():
     os.environ.setdefault('MAGOT_DEVICE', str(local))
     if args.mode == 'strong':
         return strong_main(args, dist, rank, local, world)
+    if args.config == 'C5':
+        return orf6_main(args, dist, rank, local, world)
 
     from magot_amd import _lib, engine, synth
 

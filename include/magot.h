@@ -195,6 +195,32 @@ int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* s
                           const uint64_t* pep_off, uint8_t* out);
 
 /*
+ * Six-frame translation for Sequence.get_orfs (genome.py:824-851): for each
+ * record, translate(frame=f, strand) for f = 0,1,2 and strand '-','+' in the
+ * reference's loop order.  Stream j = 6*record + 2*f + (strand == '+') holds
+ * the REAL codons only: frames 1/2 start with a junk 1-/2-base codon that
+ * trimX always drops (genome.py:809-821), so it is not emitted; frame 0 is
+ * untrimmed (the caller drops one leading 'X').  Streams start on 16-byte
+ * boundaries: stream_off (6n+1) are the padded offsets, stream_len (6n) the
+ * real residue counts; none_mask[j] = 1 where the reference returns None
+ * (len <= 2 + f).  stream_len / none_mask may be NULL.
+ */
+int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,
+                     uint64_t* stream_len, uint8_t* none_mask);
+int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
+                     const uint8_t* lut64, const uint64_t* stream_off, uint8_t* out);
+/* The same over an extraction plan's nucleotide records, kept in HBM
+ * (BASELINE configs[4], C5: gather + six-frame translation). */
+typedef struct magot_orf6 magot_orf6;
+int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_orf6** out,
+                    uint64_t* total_res);
+int magot_orf6_execute(magot_ctx* ctx, magot_orf6* o);
+int magot_orf6_fetch(magot_ctx* ctx, magot_orf6* o, uint8_t* out, uint64_t* stream_off,
+                     uint64_t* stream_len);
+int magot_orf6_time(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms);
+void magot_orf6_destroy(magot_orf6* o);
+
+/*
  * Native batch planner for gff2fasta (genome_tools.py:324-330).
  * Parses GFF3/GTF text with read_gff's rules and default arguments
  * (genome.py:242-415: '#'/8-tab acceptance, version sniffing, ID synthesis

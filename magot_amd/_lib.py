@@ -33,6 +33,8 @@ EXPORTS = (
     'magot_gff_plan', 'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
     'magot_genome_export', 'magot_genome_copy_arena', 'magot_genome_attach',
     'magot_plan_copy_outputs',
+    'magot_orf6_sizes', 'magot_orf6_batch', 'magot_plan_orf6', 'magot_orf6_execute',
+    'magot_orf6_fetch', 'magot_orf6_time', 'magot_orf6_destroy',
 )
 
 ERR_UNSUPPORTED = -5
@@ -94,6 +96,14 @@ def _declare(lib):
         'magot_genome_attach': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp,
                                                ctypes.POINTER(_vp)]),
         'magot_plan_copy_outputs': (ctypes.c_int, [_vp, _vp, _vp, _vp]),
+        'magot_orf6_sizes': (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
+        'magot_orf6_batch': (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
+        'magot_plan_orf6': (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(_vp), _u64p]),
+        'magot_orf6_execute': (ctypes.c_int, [_vp, _vp]),
+        'magot_orf6_fetch': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
+        'magot_orf6_time': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_double)]),
+        'magot_orf6_destroy': (None, [_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

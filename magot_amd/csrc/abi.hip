@@ -801,4 +801,206 @@ int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* s
   return rc;
 }
 
+// --- six-frame translation (Sequence.get_orfs, genome.py:824-851) ----------
+
+int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,
+                     uint64_t* stream_len, uint8_t* none_mask) {
+  if (!seq_off || !stream_off) {
+    set_error("magot_orf6_sizes: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  uint64_t acc = 0;
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint64_t L = seq_off[r + 1] - seq_off[r];
+    for (uint32_t f = 0; f < 3; ++f) {
+      // real codons start at 2f, 2f+3, ... (frames 1/2 emit a junk codon first)
+      const bool none = L <= 2 + f;
+      const uint64_t c = (!none && L >= 2 * f + 3) ? (L - 2 * f) / 3 : 0;
+      for (int st = 0; st < 2; ++st) {
+        const uint64_t j = 6 * r + 2 * f + st;
+        stream_off[j] = acc;  // streams start on 16-byte boundaries
+        if (stream_len) stream_len[j] = c;
+        if (none_mask) none_mask[j] = none ? 1 : 0;
+        acc += (c + 15) & ~15ull;
+      }
+    }
+  }
+  stream_off[6 * n] = acc;
+  return MAGOT_OK;
+}
+
+int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
+                     const uint8_t* lut64, const uint64_t* stream_off, uint8_t* out) {
+  if (int rc = bind(ctx)) return rc;
+  if (!seq_off || !stream_off) {
+    set_error("magot_orf6_batch: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  const uint64_t total = n ? seq_off[n] : 0, total_res = n ? stream_off[6 * n] : 0;
+  if (total_res == 0) return MAGOT_OK;
+  if (!seqs || !out) {
+    set_error("magot_orf6_batch: null buffer");
+    return MAGOT_ERR_ARG;
+  }
+  uint8_t lut[64];
+  if (lut64) std::memcpy(lut, lut64, 64);
+  else standard_lut(lut);
+  uint32_t lut16[16];
+  std::memcpy(lut16, lut, 64);
+  Carve cv;
+  const uint64_t o_in = cv.take<uint8_t>(total + 64);
+  const uint64_t o_out = cv.take<uint8_t>(total_res + 64);
+  const uint64_t o_off = cv.take<uint64_t>(n + 1);
+  const uint64_t o_soff = cv.take<uint64_t>(6 * n + 1);
+  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(total_res));
+  const uint64_t o_lut = cv.take<uint8_t>(64);
+  void* d = nullptr;
+  MAGOT_HIP_TRY(hipMalloc(&d, cv.used));
+  char* base = static_cast<char*>(d);
+  hipError_t e = hipMemcpyAsync(base + o_in, seqs, total, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(base + o_lut, lut, 64, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(base + o_off, seq_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(base + o_soff, stream_off, (6 * n + 1) * 8, hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess) {
+    uint32_t* wj = reinterpret_cast<uint32_t*>(base + o_wj);
+    launch_orf6_index(reinterpret_cast<const uint64_t*>(base + o_soff), n, wj, ctx->stream);
+    launch_orf6(reinterpret_cast<const uint8_t*>(base + o_in),
+                reinterpret_cast<const uint64_t*>(base + o_off), n,
+                reinterpret_cast<const uint64_t*>(base + o_soff), total_res, wj,
+                reinterpret_cast<const uint8_t*>(base + o_lut),
+                reinterpret_cast<uint8_t*>(base + o_out), ctx->stream);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, base + o_out, total_res, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  int rc = MAGOT_OK;
+  if (e != hipSuccess) {
+    set_error(std::string("magot_orf6_batch: ") + hipGetErrorString(e));
+    rc = MAGOT_ERR_HIP;
+  }
+  (void)hipFree(d);
+  return rc;
+}
+
+struct magot_orf6 {
+  magot_ctx* ctx = nullptr;
+  magot_plan* plan = nullptr;
+  void* arena = nullptr;
+  const uint64_t* noff = nullptr;
+  const uint64_t* soff = nullptr;
+  uint32_t* wave_j0 = nullptr;
+  uint8_t* lut_dev = nullptr;
+  uint8_t* out = nullptr;
+  uint64_t n_rec = 0, total = 0;
+  std::vector<uint64_t> host_soff;
+  uint32_t lut16[16];
+};
+
+int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_orf6** out,
+                    uint64_t* total_res) {
+  if (int rc = bind(ctx)) return rc;
+  if (!p || !out || !(p->args.outputs & MAGOT_OUT_NUC)) {
+    set_error("magot_plan_orf6: needs a plan with nucleotide output");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  std::unique_ptr<magot_orf6> o(new magot_orf6());
+  o->ctx = ctx;
+  o->plan = p;
+  o->n_rec = p->n_tx;
+  o->host_soff.resize(6 * o->n_rec + 1);
+  if (int rc = magot_orf6_sizes(p->nuc_off.data(), o->n_rec, o->host_soff.data(), nullptr, nullptr))
+    return rc;
+  o->total = o->host_soff.back();
+  uint8_t lut[64];
+  if (lut64) std::memcpy(lut, lut64, 64);
+  else standard_lut(lut);
+  std::memcpy(o->lut16, lut, 64);
+  Carve cv;
+  const uint64_t o_off = cv.take<uint64_t>(o->n_rec + 1);
+  const uint64_t o_soff = cv.take<uint64_t>(6 * o->n_rec + 1);
+  const uint64_t o_out = cv.take<uint8_t>(o->total + 64);
+  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(o->total));
+  const uint64_t o_lut = cv.take<uint8_t>(64);
+  MAGOT_HIP_TRY(hipMalloc(&o->arena, cv.used));
+  char* base = static_cast<char*>(o->arena);
+  o->noff = reinterpret_cast<const uint64_t*>(base + o_off);
+  o->soff = reinterpret_cast<const uint64_t*>(base + o_soff);
+  o->out = reinterpret_cast<uint8_t*>(base + o_out);
+  MAGOT_HIP_TRY(hipMemcpy(base + o_off, p->nuc_off.data(), (o->n_rec + 1) * 8,
+                          hipMemcpyHostToDevice));
+  MAGOT_HIP_TRY(hipMemcpy(base + o_soff, o->host_soff.data(), (6 * o->n_rec + 1) * 8,
+                          hipMemcpyHostToDevice));
+  o->wave_j0 = reinterpret_cast<uint32_t*>(base + o_wj);
+  o->lut_dev = reinterpret_cast<uint8_t*>(base + o_lut);
+  MAGOT_HIP_TRY(hipMemcpy(o->lut_dev, lut, 64, hipMemcpyHostToDevice));
+  launch_orf6_index(o->soff, o->n_rec, o->wave_j0, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (total_res) *total_res = o->total;
+  *out = o.release();
+  return MAGOT_OK;
+}
+
+int magot_orf6_execute(magot_ctx* ctx, magot_orf6* o) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o) {
+    set_error("magot_orf6_execute: null handle");
+    return MAGOT_ERR_ARG;
+  }
+  launch_orf6(o->plan->args.nuc, o->noff, o->n_rec, o->soff, o->total, o->wave_j0, o->lut_dev,
+              o->out, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  return MAGOT_OK;
+}
+
+int magot_orf6_fetch(magot_ctx* ctx, magot_orf6* o, uint8_t* out, uint64_t* stream_off,
+                     uint64_t* stream_len) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o) {
+    set_error("magot_orf6_fetch: null handle");
+    return MAGOT_ERR_ARG;
+  }
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (out && o->total) MAGOT_HIP_TRY(hipMemcpy(out, o->out, o->total, hipMemcpyDeviceToHost));
+  if (stream_off)
+    std::memcpy(stream_off, o->host_soff.data(), o->host_soff.size() * sizeof(uint64_t));
+  if (stream_len) {
+    std::vector<uint64_t> tmp(6 * o->n_rec + 1);
+    return magot_orf6_sizes(o->plan->nuc_off.data(), o->n_rec, tmp.data(), stream_len, nullptr);
+  }
+  return MAGOT_OK;
+}
+
+int magot_orf6_time(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o || !avg_ms || iters <= 0) {
+    set_error("magot_orf6_time: bad argument");
+    return MAGOT_ERR_ARG;
+  }
+  double total = 0;
+  for (int i = 0; i < iters; ++i) {
+    MAGOT_HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    launch_orf6(o->plan->args.nuc, o->noff, o->n_rec, o->soff, o->total, o->wave_j0, o->lut_dev,
+                o->out, ctx->stream);
+    MAGOT_HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    MAGOT_HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0;
+    MAGOT_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    total += ms;
+  }
+  *avg_ms = total / iters;
+  return MAGOT_OK;
+}
+
+void magot_orf6_destroy(magot_orf6* o) {
+  if (!o) return;
+  if (o->ctx) (void)hipSetDevice(o->ctx->device);
+  if (o->arena) (void)hipFree(o->arena);
+  delete o;
+}
+
 }  // extern "C"

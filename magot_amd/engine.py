@@ -259,6 +259,84 @@ def revcomp_batch(seqs, ctx=None):
     return [raw[int(off[i]):int(off[i + 1])].decode('latin-1') for i in range(len(seqs))]
 
 
+def orf6_batch(seqs, lut64=None, ctx=None):
+    """The six translations Sequence.get_orfs splits (genome.py:824-851), per
+    input: a list of 6 values in the reference's loop order (frame 0,1,2 x
+    strand '-','+'), each the trimmed ``translate()`` result or None."""
+    ctx = ctx or _lib.default_context()
+    n = len(seqs)
+    buf, off = _concat(seqs)
+    soff = np.empty(6 * n + 1, dtype=np.uint64)
+    slen = np.empty(max(6 * n, 1), dtype=np.uint64)
+    none = np.empty(max(6 * n, 1), dtype=np.uint8)
+    L = _lib.lib()
+    check(L.magot_orf6_sizes(ptr(off), n, ptr(soff), ptr(slen), ptr(none)), 'magot_orf6_sizes')
+    total = int(soff[6 * n])
+    out = np.empty(max(total, 1), dtype=np.uint8)
+    lut = np.frombuffer(bytes(lut64), dtype=np.uint8).copy() if lut64 is not None else None
+    check(L.magot_orf6_batch(ctx.handle, ptr(buf) if len(buf) else None, ptr(off), n, ptr(lut),
+                             ptr(soff), ptr(out)), 'magot_orf6_batch')
+    raw = out[:total].tobytes().decode('latin-1')
+    res = []
+    for r in range(n):
+        six = []
+        for j in range(6 * r, 6 * r + 6):
+            if none[j]:
+                six.append(None)
+                continue
+            t = raw[int(soff[j]):int(soff[j] + slen[j])]
+            if (j % 6) < 2 and t[:1] == 'X':  # frame 0: trimX (genome.py:819-821)
+                t = t[1:]
+            six.append(t)
+        res.append(six)
+    return res
+
+
+class Orf6Plan(object):
+    """Six-frame translation of an ExtractionPlan's records, in HBM
+    (magot_plan_orf6): BASELINE configs[4] (C5)."""
+
+    def __init__(self, plan, lut64=None):
+        self.plan = plan
+        self.ctx = plan.ctx
+        lut = np.frombuffer(bytes(lut64), dtype=np.uint8).copy() if lut64 is not None else None
+        h = ctypes.c_void_p()
+        tot = ctypes.c_uint64()
+        check(_lib.lib().magot_plan_orf6(self.ctx.handle, plan.handle, ptr(lut), ctypes.byref(h),
+                                         ctypes.byref(tot)), 'magot_plan_orf6')
+        self.handle = h
+        self.total = tot.value
+
+    def execute(self):
+        check(_lib.lib().magot_orf6_execute(self.ctx.handle, self.handle), 'magot_orf6_execute')
+
+    def fetch(self):
+        """(padded residue bytes, stream offsets 6n+1 (16-aligned), real stream lengths 6n)."""
+        out = np.empty(max(self.total, 1), dtype=np.uint8)
+        soff = np.empty(6 * self.plan.n_tx + 1, dtype=np.uint64)
+        slen = np.empty(max(6 * self.plan.n_tx, 1), dtype=np.uint64)
+        check(_lib.lib().magot_orf6_fetch(self.ctx.handle, self.handle, ptr(out), ptr(soff),
+                                          ptr(slen)), 'magot_orf6_fetch')
+        return out[:self.total], soff, slen[:6 * self.plan.n_tx]
+
+    def time(self, iters):
+        ms = ctypes.c_double()
+        check(_lib.lib().magot_orf6_time(self.ctx.handle, self.handle, int(iters),
+                                         ctypes.byref(ms)), 'magot_orf6_time')
+        return ms.value
+
+    def close(self):
+        if getattr(self, 'handle', None):
+            _lib.lib().magot_orf6_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
     """Untrimmed Sequence.translate (genome.py:795-822) residues per input, or None
     where the reference returns None.  The caller applies trimX."""
@@ -292,4 +370,4 @@ def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
 
 
 __all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'OUT_NUC',
-           'OUT_PEP', 'MagotError', 'GffPlan']
+           'OUT_PEP', 'MagotError', 'GffPlan', 'orf6_batch', 'Orf6Plan']

@@ -164,10 +164,8 @@ class Sequence(str):
 
     def get_orfs(self, longest=False, strand='both', from_atg=False):
         """genome.py:824-851; the ``strand`` argument is shadowed (genome.py:830)."""
-        jobs = [(f, s) for f in (0, 1, 2) for s in ('-', '+')]
-        peps = engine.translate_batch([str(self)] * 6, [f for f, _ in jobs],
-                                      [s for _, s in jobs])
-        return _orfs_from_translations([_trim(p, True) for p in peps], longest, from_atg)
+        peps = engine.orf6_batch([str(self)])[0]  # six-frame kernel, loop order kept
+        return _orfs_from_translations(peps, longest, from_atg)
 
 
 def _trim(res, trimX):

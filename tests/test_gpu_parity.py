@@ -347,3 +347,51 @@ def test_degenerate_intervals_vs_c_oracle():
     w.ex_start[last] = np.maximum(clen - 3, w.ex_start[last])
     w.ex_len[last] = 10
     check_against_oracle(w)
+
+
+# ---------------------------------------------------------------------------
+# Six-frame translation (Sequence.get_orfs, genome.py:824-851): orf6_kernel
+# ---------------------------------------------------------------------------
+
+def _oracle_six(s):
+    return [mo.translate(s, frame=f, strand=st) for f in (0, 1, 2) for st in ('-', '+')]
+
+
+def test_orf6_batch_vs_oracle():
+    rng = np.random.default_rng(41)
+    alphabet = np.frombuffer(b'ACGTACGTACGTacgtNnRY-*', dtype=np.uint8)
+    seqs = []
+    for L in list(range(0, 24)) + [int(x) for x in rng.integers(24, 3000, size=300)]:
+        seqs.append(alphabet[rng.integers(0, len(alphabet), size=L)].tobytes().decode('latin-1'))
+    got = engine.orf6_batch(seqs)
+    for s, six in zip(seqs, got):
+        assert six == _oracle_six(s), s[:40]
+
+
+def test_orf6_over_extraction_plan_vs_oracle():
+    """C5 shape at small size: gather + six-frame translation, all in HBM."""
+    w = synth.make('small', seed=43, genome_bases=1_000_000, n_tx=400, iupac_rate=2e-3)
+    dev = engine.DeviceGenome(w.contigs())
+    ex, tx = w.plan_tables()
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    nuc, noff, _, _ = plan.run()
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    raw = out.tobytes().decode('latin-1')
+    for r in range(len(tx)):
+        s = nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1')
+        want = _oracle_six(s)
+        for k in range(6):
+            j = 6 * r + k
+            assert int(soff[j]) % 16 == 0
+            t = raw[int(soff[j]):int(soff[j] + slen[j])]
+            if k < 2 and t[:1] == 'X':
+                t = t[1:]
+            if want[k] is None:
+                assert t == ''
+            else:
+                assert t == want[k], (r, k)
+    o6.close()
+    plan.close()
+    dev.close()
