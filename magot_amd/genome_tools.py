@@ -4,6 +4,9 @@
            [longest=True] [genomic=True] [from_exons=True] [order=py2|insertion]
            [native=False]
     python -m magot_amd.genome_tools cds2pep <cds.fasta>
+    python -m magot_amd.genome_tools extract_upstream_downstream <fasta> <gff> <length> up|down
+           [feature_type=gene] [namefrom=ID] [truncate_names=True]
+    python -m magot_amd.genome_tools coords2fasta <fasta> <seqid> <start> <stop> [truncate_names=False]
 
 Arguments follow the reference's CLI convention (genome_tools.py:25-45):
 positional values, then ``key=value`` pairs, all strings.  The reference
@@ -17,6 +20,8 @@ Python-3 order.
 
 import ast
 import sys
+
+import numpy as np
 
 from . import engine
 from . import genome
@@ -128,7 +133,82 @@ def cds2pep(fasta_file):
         raise failure
 
 
-TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep}
+def _gather(seqs, intervals):
+    """Bytes of (contig index, start, length, rc) intervals: one kernel launch."""
+    if not intervals:
+        return []
+    ex = np.zeros(len(intervals), dtype=engine.EXON_DTYPE)
+    for i, (c, st, ln, rc) in enumerate(intervals):
+        ex[i] = ((st | (1 << 63)) if rc else st, c, ln)
+    tx = np.zeros(len(intervals), dtype=engine.TX_DTYPE)
+    tx['exon_begin'] = np.arange(len(intervals))
+    tx['n_exons'] = 1
+    plan = engine.ExtractionPlan(seqs.device(), ex, tx, engine.OUT_NUC)
+    try:
+        nuc, noff, _, _ = plan.run()
+    finally:
+        plan.close()
+    raw = nuc.tobytes().decode('latin-1')
+    return [raw[int(noff[i]):int(noff[i + 1])] for i in range(len(intervals))]
+
+
+def extract_upstream_downstream(genome_sequence, gff, sequence_length, stream,
+                                feature_type='gene', namefrom='ID', truncate_names='True'):
+    """genome_tools.py:457-480: the `sequence_length` bases up- or downstream of
+    every `feature_type` line, strand-aware, gathered on the GPU in one batch.
+    Reference quirks kept: 'down' on '+' and 'up' on '-' are reverse
+    complemented; a strand other than '+'/'-' reuses the previous line's
+    sequence (or raises UnboundLocalError); only full-length windows print."""
+    seqs = genome.GenomeSequence(genome_sequence, truncate_names=_literal(truncate_names))
+    n = int(sequence_length)
+    index = {name: i for i, name in enumerate(seqs)}
+    current = None
+    items = []
+    with open(gff, 'rb') as fh:
+        lines = fh.read().decode('latin-1').split('\n')
+    lines = [ln + '\n' for ln in lines[:-1]] + ([lines[-1]] if lines[-1] else [])
+    for line in lines:
+        if line.count('\t') > 5 and line[0] != '#':
+            fields = line.split('\t')
+            if fields[2] == feature_type:
+                name = None
+                coords = sorted([int(fields[3]), int(fields[4])])
+                for attribute in fields[-1].split(';'):
+                    if namefrom == attribute.split('=')[0]:
+                        name = attribute.split('=')[1].replace('\r', '').replace('\n', '')
+                if name is None:
+                    name = 'seq' + str(len(items))
+                if stream == 'up' and fields[6] == '+' or stream == 'down' and fields[6] == '-':
+                    stop = coords[0] - 1
+                    st, ln = genome._slice_interval(seqs[fields[0]], stop - n, stop)
+                    current = (index[fields[0]], st, ln, False)
+                elif stream == 'down' and fields[6] == '+' or stream == 'up' and fields[6] == '-':
+                    start = coords[1]
+                    st, ln = genome._slice_interval(seqs[fields[0]], start, start + n)
+                    current = (index[fields[0]], st, ln, True)
+                if current is None:
+                    raise UnboundLocalError(
+                        "local variable 'sequence' referenced before assignment")
+                if current[2] == n:
+                    items.append((name, current))
+    texts = _gather(seqs, [iv for _, iv in items])
+    _write('\n'.join('>' + name + '\n' + t for (name, _), t in zip(items, texts)) + '\n')
+
+
+def coords2fasta(fasta_file, seqid, start, stop, truncate_names='False'):
+    """genome_tools.py:656-661: header, then contig[start-1:stop] (Python slice
+    rules) gathered on the GPU."""
+    _write('>' + seqid + ':' + start + '-' + stop + '\n')
+    seqs = genome.Genome(fasta_file, truncate_names=_literal(truncate_names)).genome_sequence
+    contig = seqs[seqid]
+    st, ln = genome._slice_interval(contig, int(start) - 1, int(stop))
+    index = {name: i for i, name in enumerate(seqs)}
+    _write(_gather(seqs, [(index[seqid], st, ln, False)])[0] + '\n')
+
+
+TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep,
+         'extract_upstream_downstream': extract_upstream_downstream,
+         'coords2fasta': coords2fasta}
 
 
 def parse_argv(argv):

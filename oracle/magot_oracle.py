@@ -614,3 +614,59 @@ def cds2pep(fasta):
             work = work + line
     outl.append(str(translate(work)))
     return '\n'.join(outl) + '\n'
+
+
+# ---------------------------------------------------------------------------
+# Locus extraction: genome_tools.py:457-480 and :656-661
+# ---------------------------------------------------------------------------
+
+def extract_upstream_downstream(genome_sequence, gff_path, sequence_length, stream,
+                                feature_type='gene', namefrom='ID', truncate_names='True',
+                                out=None):
+    """genome_tools.py:457-480.  Returns the printed text; exceptions propagate
+    after whatever the reference would have printed (nothing: it prints once,
+    at the end)."""
+    seqs = read_fasta(genome_sequence, truncate_names=truncate_names == 'True')
+    output_seqs = []
+    sequence = None
+    bound = False
+    with open(gff_path, 'rb') as fh:
+        text = fh.read().decode('latin-1')
+    for line in _split_keep_nl(text):
+        if line.count('\t') > 5 and line[0] != '#':
+            fields = line.split('\t')
+            if fields[2] == feature_type:
+                name = None
+                coords = [int(fields[3]), int(fields[4])]
+                coords.sort()
+                for attribute in fields[-1].split(';'):
+                    if namefrom == attribute.split('=')[0]:
+                        name = attribute.split('=')[1].replace('\r', '').replace('\n', '')
+                if name is None:
+                    name = 'seq' + str(len(output_seqs))
+                n = int(sequence_length)
+                if stream == 'up' and fields[6] == '+' or stream == 'down' and fields[6] == '-':
+                    stop = coords[0] - 1
+                    sequence = seqs[fields[0]][stop - n:stop]
+                    bound = True
+                elif stream == 'down' and fields[6] == '+' or stream == 'up' and fields[6] == '-':
+                    start = coords[1]
+                    sequence = reverse_complement(seqs[fields[0]][start:start + n])
+                    bound = True
+                if not bound:
+                    raise UnboundLocalError("local variable 'sequence' referenced before "
+                                            "assignment")
+                if len(sequence) == n:
+                    output_seqs.append('>' + name + '\n' + sequence)
+    return '\n'.join(output_seqs) + '\n'
+
+
+def coords2fasta(fasta_file, seqid, start, stop, truncate_names='False', out=None):
+    """genome_tools.py:656-661: (text printed, exception or None)."""
+    text = '>' + seqid + ':' + start + '-' + stop + '\n'
+    try:
+        seq = read_fasta(fasta_file, truncate_names=truncate_names == 'True')[seqid][
+            int(start) - 1:int(stop)]
+    except Exception as e:  # noqa: BLE001 -- the header is printed before the lookup
+        return text, e
+    return text + seq + '\n', None

@@ -14,6 +14,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   edge_cases.json get_fasta edge cases incl. stdout/exception
   fixtures.json   hashes of whole-file gff2fasta outputs on the shipped data
   synth_small.json hashes of gff2fasta on the seeded small synthetic
+  loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -237,8 +238,73 @@ def make_synth(ref):
     return out
 
 
+LOCUS_GENOME = ('>c1 first contig\nACGTACGTAAccggttNNRYacgtACGTAAATTTGGGCCCAATTGGCC\n'
+                '>c2\nGGGAAATTTCCCgggaaatttcccAAACCCGGGTTT\n')
+LOCUS_GFF = ''.join([
+    'c1\tt\tgene\t10\t20\t.\t+\t.\tID=g1;Name=alpha\n',
+    'c1\tt\tgene\t3\t8\t.\t-\t.\tID=g2\n',
+    'c1\tt\tgene\t30\t40\t.\t-\t.\tName=gamma\n',
+    '#c1\tt\tgene\t1\t5\t.\t+\t.\tID=hidden\n',
+    'c2\tt\tgene\t20\t12\t.\t+\t.\tID=g4\n',
+    'c2\tt\tmRNA\t12\t20\t.\t+\t.\tID=m4;Parent=g4\n',
+    'c2\tt\tgene\t2\t5\t.\t+\t.\tID=g5\n',
+])
+
+
+def make_locus(ref):
+    """genome_tools.extract_upstream_downstream (:457-480) and coords2fasta
+    (:656-661) of the reference, stdout captured (the shapes SURVEY 8(f)4)."""
+    sys.path.insert(0, PY3)
+    import genome_tools as rt
+    import tempfile
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        gff_path = os.path.join(td, 'loci.gff')
+        with open(gff_path, 'w') as fh:
+            fh.write(LOCUS_GFF)
+        fa_path = os.path.join(td, 'loci.fa')
+        with open(fa_path, 'w') as fh:
+            fh.write(LOCUS_GENOME)
+        ob_fa = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
+        ob_gff = goldlib.path('O.biroi_NCBIrefseq_gff3Subset.gff')
+        runs = []
+        for stream in ('up', 'down'):
+            for n in ('3', '6', '12'):
+                for ft in ('gene', 'mRNA'):
+                    for nf in ('ID', 'Name'):
+                        runs.append(('small', fa_path, gff_path, n, stream, ft, nf, 'True'))
+            for n in ('50', '300'):
+                for ft in ('gene', 'CDS'):
+                    runs.append(('obiroi', ob_fa, ob_gff, n, stream, ft, 'ID', 'True'))
+        runs.append(('obiroi-untruncated', ob_fa, ob_gff, '50', 'up', 'gene', 'ID', 'False'))
+        for tag, fa, gff, n, stream, ft, nf, tr in runs:
+            key = 'updown/%s/%s/%s/%s/%s/%s' % (tag, stream, n, ft, nf, tr)
+            res, exc, so = call(lambda: rt.extract_upstream_downstream(fa, gff, n, stream, ft, nf, tr))
+            d = digest(None, exc, so)
+            if len(so) < 400:
+                d['stdout'] = so
+            out[key] = d
+        for seqid, a, b, tr in [('c1', '1', '10'), ('c1', '0', '5'), ('c1', '40', '99'),
+                                ('c2', '5', '3'), ('c1 first contig', '2', '4'), ('c1', '2', '4'),
+                                ('zz', '1', '2')] and [(x[0], x[1], x[2], t) for x in
+                                                       [('c1', '1', '10'), ('c1', '0', '5'),
+                                                        ('c1', '40', '99'), ('c2', '5', '3'),
+                                                        ('c1 first contig', '2', '4'),
+                                                        ('c1', '2', '4'), ('zz', '1', '2')]
+                                                       for t in ('False', 'True')]:
+            key = 'coords/%s/%s/%s/%s' % (seqid, a, b, tr)
+            res, exc, so = call(lambda: rt.coords2fasta(fa_path, seqid, a, b, tr))
+            d = digest(None, exc, so)
+            d['stdout'] = so
+            out[key] = d
+    out['_inputs'] = {'genome': LOCUS_GENOME, 'gff': LOCUS_GFF}
+    return out
+
+
 def main():
     ref = reference_module()
+    with open(os.path.join(HERE, 'loci.json'), 'w') as fh:
+        json.dump(make_locus(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'kat.json'), 'w') as fh:
         json.dump(make_kat(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'edge_cases.json'), 'w') as fh:

@@ -1,0 +1,109 @@
+"""Locus extraction: genome_tools.extract_upstream_downstream
+(genome_tools.py:457-480) and coords2fasta (:656-661).
+
+tests/golden/loci.json holds the REFERENCE's own stdout / exception for every
+case (tests/golden/make_golden.py).  CPU: the oracle restatement reproduces
+them.  GPU (marked): the drop-in CLI functions, which gather every window with
+one extraction-kernel launch, reproduce them byte for byte.
+"""
+import contextlib
+import hashlib
+import io
+import json
+import os
+
+import pytest
+
+import goldlib
+from oracle import magot_oracle as mo
+
+GOLD = json.load(open(os.path.join(goldlib.HERE, 'loci.json')))
+
+
+def _sha(s):
+    return hashlib.sha256(s.encode('latin-1')).hexdigest()
+
+
+@pytest.fixture(scope='module')
+def small(tmp_path_factory):
+    d = tmp_path_factory.mktemp('loci')
+    fa, gff = d / 'loci.fa', d / 'loci.gff'
+    fa.write_text(GOLD['_inputs']['genome'])
+    gff.write_text(GOLD['_inputs']['gff'])
+    return str(fa), str(gff)
+
+
+def _updown_cases():
+    for key in sorted(GOLD):
+        if key.startswith('updown/'):
+            yield key
+
+
+def _coords_cases():
+    for key in sorted(GOLD):
+        if key.startswith('coords/'):
+            yield key
+
+
+def _paths(tag, small):
+    if tag == 'small':
+        return small
+    return (goldlib.path('O.biroi_refseqGenomeSubset.fasta'),
+            goldlib.path('O.biroi_NCBIrefseq_gff3Subset.gff'))
+
+
+@pytest.mark.parametrize('key', list(_updown_cases()))
+def test_oracle_updown_matches_reference(small, key):
+    _, tag, stream, n, ft, nf, tr = key.split('/')
+    fa, gff = _paths(tag, small)
+    want = GOLD[key]
+    try:
+        text = mo.extract_upstream_downstream(fa, gff, n, stream, ft, nf, tr)
+        exc = None
+    except Exception as e:  # noqa: BLE001
+        text, exc = '', type(e).__name__
+    assert exc == want['exc']
+    assert _sha(text) == want['stdout_sha256']
+
+
+@pytest.mark.parametrize('key', list(_coords_cases()))
+def test_oracle_coords2fasta_matches_reference(small, key):
+    _, seqid, a, b, tr = key.split('/')
+    text, exc = mo.coords2fasta(small[0], seqid, a, b, tr)
+    assert (type(exc).__name__ if exc else None) == GOLD[key]['exc']
+    assert text == GOLD[key]['stdout']
+
+
+def _run_cli(fn, *args):
+    buf = io.BytesIO()
+    out = io.TextIOWrapper(buf, encoding='latin-1', write_through=True)
+    exc = None
+    with contextlib.redirect_stdout(out):
+        try:
+            fn(*args)
+        except Exception as e:  # noqa: BLE001
+            exc = type(e).__name__
+    out.flush()
+    return buf.getvalue().decode('latin-1'), exc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('key', list(_updown_cases()))
+def test_gpu_updown_matches_reference(small, key):
+    from magot_amd import genome_tools
+    _, tag, stream, n, ft, nf, tr = key.split('/')
+    fa, gff = _paths(tag, small)
+    text, exc = _run_cli(genome_tools.extract_upstream_downstream, fa, gff, n, stream, ft, nf, tr)
+    assert exc == GOLD[key]['exc']
+    if exc is None:
+        assert _sha(text) == GOLD[key]['stdout_sha256']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('key', list(_coords_cases()))
+def test_gpu_coords2fasta_matches_reference(small, key):
+    from magot_amd import genome_tools
+    _, seqid, a, b, tr = key.split('/')
+    text, exc = _run_cli(genome_tools.coords2fasta, small[0], seqid, a, b, tr)
+    assert exc == GOLD[key]['exc']
+    assert text == GOLD[key]['stdout']
