@@ -105,6 +105,25 @@ void magot_ctx_destroy(magot_ctx* ctx);
  */
 int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
                       uint32_t n_contigs, magot_genome** out);
+/*
+ * Read FASTA text (GenomeSequence, genome.py:854-877, incl. truncate_names)
+ * natively and pack it like magot_genome_load.  MAGOT_ERR_UNSUPPORTED for
+ * headers whose whitespace split differs between the reference's Python 2
+ * byte strings and Python 3 (bytes >= 0x80, 0x1c-0x1f) or that are empty
+ * under truncate_names: the caller then uses the Python reader.
+ * magot_genome_contigs: contig count, lengths and NUL-separated names (names
+ * only for genomes read by magot_genome_load_fasta; NULL buffers = sizes).
+ */
+int magot_genome_load_fasta(magot_ctx* ctx, const char* text, uint64_t len, int truncate_names,
+                            magot_genome** out);
+int magot_genome_contigs(const magot_genome* g, uint32_t* n, uint64_t* lens, char* names,
+                         uint64_t names_cap, uint64_t* names_len);
+/* Host-only: the same FASTA reader into caller buffers (first call with NULL
+ * buffers for the count, lengths and name bytes; lens needs n entries). */
+int magot_fasta_read(const char* text, uint64_t len, int truncate_names, uint32_t* n,
+                     uint64_t* lens, char* names, uint64_t names_cap, uint64_t* names_len,
+                     uint8_t* seqs, uint64_t seqs_cap);
+
 /* Sizes of a loaded genome: total bases, exception runs, device bytes held. */
 int magot_genome_stats(const magot_genome* g, uint64_t* total_bases, uint64_t* n_exc_runs,
                        uint64_t* device_bytes);

@@ -35,6 +35,7 @@ EXPORTS = (
     'magot_plan_copy_outputs',
     'magot_orf6_sizes', 'magot_orf6_batch', 'magot_plan_orf6', 'magot_orf6_execute',
     'magot_orf6_fetch', 'magot_orf6_time', 'magot_orf6_destroy',
+    'magot_genome_load_fasta', 'magot_genome_contigs', 'magot_fasta_read',
 )
 
 ERR_UNSUPPORTED = -5
@@ -104,6 +105,13 @@ def _declare(lib):
         'magot_orf6_time': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_double)]),
         'magot_orf6_destroy': (None, [_vp]),
+        'magot_genome_load_fasta': (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_uint64,
+                                                   ctypes.c_int, ctypes.POINTER(_vp)]),
+        'magot_genome_contigs': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32), _vp, _vp,
+                                                ctypes.c_uint64, _u64p]),
+        'magot_fasta_read': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
+                                            ctypes.POINTER(ctypes.c_uint32), _vp, _vp,
+                                            ctypes.c_uint64, _u64p, _vp, ctypes.c_uint64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

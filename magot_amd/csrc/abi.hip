@@ -50,6 +50,7 @@ struct magot_genome {
   ExcRun* runs = nullptr;
   uint32_t* dir = nullptr;
   std::vector<uint64_t> contig_base, contig_len;
+  std::vector<std::string> names;  // contig names (magot_genome_load_fasta)
   std::vector<ExcRun> host_runs;   // host copies for per-interval exception flags
   std::vector<uint32_t> host_dir;
   uint64_t extent = 0, total_bases = 0, n_runs = 0;
@@ -257,6 +258,58 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
   g->extent = hp.extent;
   g->total_bases = hp.extent - kOrigin;
   *out = g.release();
+  return MAGOT_OK;
+}
+
+int magot_genome_load_fasta(magot_ctx* ctx, const char* text, uint64_t len, int truncate_names,
+                            magot_genome** out) {
+  if (int rc = bind(ctx)) return rc;
+  if (!out || (len && !text)) {
+    set_error("magot_genome_load_fasta: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  std::vector<std::string> names, seqs;
+  if (int rc = parse_fasta(text, len, truncate_names != 0, &names, &seqs)) {
+    set_error("magot_genome_load_fasta: header needs the Python reader");
+    return rc;
+  }
+  std::vector<const uint8_t*> ptrs(seqs.size());
+  std::vector<uint64_t> lens(seqs.size());
+  for (size_t i = 0; i < seqs.size(); ++i) {
+    ptrs[i] = reinterpret_cast<const uint8_t*>(seqs[i].data());
+    lens[i] = seqs[i].size();
+  }
+  magot_genome* g = nullptr;
+  if (int rc = magot_genome_load(ctx, ptrs.data(), lens.data(), (uint32_t)seqs.size(), &g))
+    return rc;
+  g->names = std::move(names);
+  *out = g;
+  return MAGOT_OK;
+}
+
+int magot_genome_contigs(const magot_genome* g, uint32_t* n, uint64_t* lens, char* names,
+                         uint64_t names_cap, uint64_t* names_len) {
+  if (!g || !n) {
+    set_error("magot_genome_contigs: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *n = (uint32_t)g->contig_len.size();
+  if (lens) std::memcpy(lens, g->contig_len.data(), g->contig_len.size() * 8);
+  uint64_t need = 0;
+  for (const auto& s : g->names) need += s.size() + 1;
+  if (names_len) *names_len = need;
+  if (names) {
+    if (names_cap < need) {
+      set_error("magot_genome_contigs: names buffer too small");
+      return MAGOT_ERR_ARG;
+    }
+    for (const auto& s : g->names) {
+      std::memcpy(names, s.data(), s.size());
+      names += s.size();
+      *names++ = '\0';
+    }
+  }
   return MAGOT_OK;
 }
 

@@ -46,6 +46,11 @@ struct HostPacked {
   uint64_t extent = 0;            // first coordinate past the last contig
 };
 
+// FASTA text -> (names, sequences) with GenomeSequence semantics (fasta.cpp);
+// MAGOT_ERR_UNSUPPORTED for headers only the Python reader handles exactly.
+int parse_fasta(const char* text, uint64_t n, bool truncate, std::vector<std::string>* names,
+                std::vector<std::string>* seqs);
+
 // Packs raw contig bytes (multi-threaded host code, pack.cpp).
 void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, HostPacked* out);
 

@@ -104,6 +104,70 @@ class DeviceGenome(object):
             pass
 
 
+def fasta_read(text, truncate_names=False):
+    """Native GenomeSequence reader (magot_fasta_read): [(name, bytes)], or None
+    when a header needs the Python reader.  Host only."""
+    L = _lib.lib()
+    data = _as_bytes(text)
+    n = ctypes.c_uint32()
+    nl = ctypes.c_uint64()
+    rc = L.magot_fasta_read(data, len(data), int(bool(truncate_names)), ctypes.byref(n), None,
+                            None, 0, ctypes.byref(nl), None, 0)
+    if rc == _lib.ERR_UNSUPPORTED:
+        return None
+    check(rc, 'magot_fasta_read')
+    lens = np.zeros(max(n.value, 1), dtype=np.uint64)
+    names = np.zeros(max(nl.value, 1), dtype=np.uint8)
+    seqs = np.zeros(max(int(lens.sum()), 1), dtype=np.uint8)
+    check(L.magot_fasta_read(data, len(data), int(bool(truncate_names)), ctypes.byref(n),
+                             ptr(lens), ptr(names), nl.value, ctypes.byref(nl), None, 0),
+          'magot_fasta_read')
+    seqs = np.zeros(max(int(lens[:n.value].sum()), 1), dtype=np.uint8)
+    check(L.magot_fasta_read(data, len(data), int(bool(truncate_names)), ctypes.byref(n),
+                             ptr(lens), ptr(names), nl.value, ctypes.byref(nl), ptr(seqs),
+                             len(seqs)), 'magot_fasta_read')
+    nms = names[:nl.value].tobytes().split(b'\0')[:n.value]
+    out, o = [], 0
+    for i in range(n.value):
+        out.append((nms[i].decode('latin-1'), seqs[o:o + int(lens[i])].tobytes()))
+        o += int(lens[i])
+    return out
+
+
+class FastaGenome(DeviceGenome):
+    """A FASTA file read and packed natively (magot_genome_load_fasta): the
+    batch path's GenomeSequence, without Python strings.  ``None`` from
+    ``load`` when a header needs the Python reader."""
+
+    @classmethod
+    def load(cls, text, truncate_names=False, ctx=None):
+        L = _lib.lib()
+        self = cls.__new__(cls)
+        self.ctx = ctx or _lib.default_context()
+        self._keepalive = None
+        data = _as_bytes(text)
+        h = ctypes.c_void_p()
+        rc = L.magot_genome_load_fasta(self.ctx.handle, data, len(data), int(bool(truncate_names)),
+                                       ctypes.byref(h))
+        if rc == _lib.ERR_UNSUPPORTED:
+            return None
+        check(rc, 'magot_genome_load_fasta')
+        self.handle = h
+        n = ctypes.c_uint32()
+        nl = ctypes.c_uint64()
+        check(L.magot_genome_contigs(h, ctypes.byref(n), None, None, 0, ctypes.byref(nl)),
+              'magot_genome_contigs')
+        lens = np.zeros(max(n.value, 1), dtype=np.uint64)
+        names = np.zeros(max(nl.value, 1), dtype=np.uint8)
+        check(L.magot_genome_contigs(h, ctypes.byref(n), ptr(lens), ptr(names), nl.value,
+                                     ctypes.byref(nl)), 'magot_genome_contigs')
+        self.names = [x.decode('latin-1') for x in names[:nl.value].tobytes().split(b'\0')[:n.value]]
+        self.index = {nm: i for i, nm in enumerate(self.names)}
+        self.lengths = lens[:n.value]
+        self._stats()
+        return self
+
+
 class ExtractionPlan(object):
     """Interval table -> device plan (magot_plan_create).
 
@@ -370,4 +434,5 @@ def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
 
 
 __all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'OUT_NUC',
-           'OUT_PEP', 'MagotError', 'GffPlan', 'orf6_batch', 'Orf6Plan']
+           'OUT_PEP', 'MagotError', 'GffPlan', 'orf6_batch', 'Orf6Plan', 'fasta_read',
+           'FastaGenome']

@@ -73,15 +73,19 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order):
     """The gff2fasta text via the native planner, or None when it declines."""
     if order not in ('py2', 'insertion'):
         raise ValueError("order must be 'insertion' or 'py2'")
-    seqs = genome.GenomeSequence(genome_sequence)
-    names = list(seqs)
+    # the FASTA is read and packed natively; Python reader for unusual headers
+    dev = engine.FastaGenome.load(genome.read_bytes(genome_sequence))
+    if dev is None:
+        seqs = genome.GenomeSequence(genome_sequence)
+        dev = seqs.device()
+    names = dev.names
     protein = seq_type == 'protein'
-    plan = engine.GffPlan.build(genome.read_bytes(gff), names,
-                                [len(seqs[n]) for n in names], protein=protein, order=order)
+    plan = engine.GffPlan.build(genome.read_bytes(gff), names, [int(x) for x in dev.lengths],
+                                protein=protein, order=order)
     if plan is None:
         return None
     try:
-        ex = engine.ExtractionPlan(seqs.device(), plan.exons, plan.txs,
+        ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                    engine.OUT_PEP if protein else engine.OUT_NUC)
         try:
             nuc, noff, pep, poff = ex.run()

@@ -38,18 +38,15 @@ def main():
     t_gen = time.perf_counter() - t
     ph = {}
     t0 = time.perf_counter()
-    seqs = genome.GenomeSequence(fa)
-    ph['fasta_parse'] = time.perf_counter() - t0
+    dev = engine.FastaGenome.load(genome.read_bytes(fa))
+    ph['fasta_read_pack_h2d_native'] = time.perf_counter() - t0
     t = time.perf_counter()
-    names = list(seqs)
+    names = dev.names
     protein = a.seq_type == 'protein'
-    plan = engine.GffPlan.build(genome.read_bytes(gf), names,
-                                [len(seqs[n]) for n in names], protein=protein, order=a.order)
+    plan = engine.GffPlan.build(genome.read_bytes(gf), names, [int(x) for x in dev.lengths],
+                                protein=protein, order=a.order)
     ph['gff_read_and_plan_native'] = time.perf_counter() - t
     assert plan is not None
-    t = time.perf_counter()
-    dev = seqs.device()
-    ph['genome_pack_h2d'] = time.perf_counter() - t
     t = time.perf_counter()
     ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                engine.OUT_PEP if protein else engine.OUT_NUC)
