@@ -15,14 +15,17 @@
 // reproduces those diagnostics exactly.  This file never touches sequence
 // bytes: the extraction itself is the HIP kernel's.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -46,6 +49,19 @@ struct Table {
 };
 
 struct Unsupported {};  // a diagnostic path of the reference: use the object path
+
+// The first exception a worker thread caught, rethrown by the caller.
+struct FirstError {
+  std::mutex mu;
+  std::exception_ptr err;
+  void set() {
+    std::lock_guard<std::mutex> g(mu);
+    if (!err) err = std::current_exception();
+  }
+  void rethrow() {
+    if (err) std::rethrow_exception(err);
+  }
+};
 
 using sv = std::string_view;
 
@@ -71,8 +87,8 @@ struct Pool {
   size_t left = 0;
   char* cur = nullptr;
   std::vector<sv> strs;
-  std::vector<uint32_t> slots{std::vector<uint32_t>(64, 0)};  // id + 1, 0 = empty
-  std::vector<uint32_t> tags{std::vector<uint32_t>(64, 0)};   // hash bits for quick rejects
+  // slot word: (hash bits for quick rejects) << 32 | (id + 1); 0 = empty
+  std::vector<uint64_t> slots{std::vector<uint64_t>(64, 0)};
 
   void reserve(size_t n) {
     size_t cap = 64;
@@ -92,46 +108,46 @@ struct Pool {
     left -= s.size();
     return out;
   }
+  static uint64_t word(uint64_t h, uint32_t id) { return (h >> 32 << 32) | (id + 1ull); }
   void rehash(size_t cap) {
-    std::vector<uint32_t> ns(cap, 0), nt(cap, 0);
+    std::vector<uint64_t> ns(cap, 0);
     const size_t mask = cap - 1;
     for (uint32_t id = 0; id < strs.size(); ++id) {
       const uint64_t h = hash_sv(strs[id]);
       size_t i = h & mask;
       while (ns[i]) i = (i + 1) & mask;
-      ns[i] = id + 1;
-      nt[i] = (uint32_t)(h >> 32);
+      ns[i] = word(h, id);
     }
     slots.swap(ns);
-    tags.swap(nt);
   }
   // slot of s (occupied when found, else the empty slot where it goes)
   size_t probe(sv s, uint64_t h) const {
     const size_t mask = slots.size() - 1;
     size_t i = h & mask;
-    const uint32_t tg = (uint32_t)(h >> 32);
+    const uint64_t tg = h >> 32;
     for (;;) {
-      const uint32_t v = slots[i];
-      if (!v || (tags[i] == tg && strs[v - 1] == s)) return i;
+      const uint64_t v = slots[i];
+      if (!v || ((v >> 32) == tg && strs[(uint32_t)v - 1] == s)) return i;
       i = (i + 1) & mask;
     }
   }
-  int64_t find(sv s) const {
-    const uint32_t v = slots[probe(s, hash_sv(s))];
-    return v ? (int64_t)v - 1 : -1;
+  int64_t find(sv s) const { return find(s, hash_sv(s)); }
+  int64_t find(sv s, uint64_t h) const {
+    const uint64_t v = slots[probe(s, h)];
+    return v ? (int64_t)(uint32_t)v - 1 : -1;
   }
-  uint32_t intern(sv s) {
-    const uint64_t h = hash_sv(s);
+  void prefetch(uint64_t h) const { __builtin_prefetch(&slots[h & (slots.size() - 1)]); }
+  uint32_t intern(sv s) { return intern(s, hash_sv(s)); }
+  uint32_t intern(sv s, uint64_t h) {
     size_t i = probe(s, h);
-    if (slots[i]) return slots[i] - 1;
+    if (slots[i]) return (uint32_t)slots[i] - 1;
     const uint32_t id = (uint32_t)strs.size();
     strs.push_back(store(s));
     if (2 * strs.size() > slots.size()) {
       rehash(slots.size() * 2);
       return id;
     }
-    slots[i] = id + 1;
-    tags[i] = (uint32_t)(h >> 32);
+    slots[i] = word(h, id);
     return id;
   }
 };
@@ -154,8 +170,9 @@ struct Model {
     for (const char* t : {"gene", "transcript", "CDS", "UTR"}) table(t);
   }
 
-  uint32_t id(sv s) {
-    const uint32_t k = ids.intern(s);
+  uint32_t id(sv s) { return id(s, hash_sv(s)); }
+  uint32_t id(sv s, uint64_t h) {
+    const uint32_t k = ids.intern(s, h);
     while (id_types.size() < ids.strs.size()) {
       id_types.push_back(0);
       first_table.push_back(0);
@@ -281,217 +298,419 @@ struct Tags {  // a dict: later assignments update the value in place
   }
 };
 
-void read_gff(Model& M, const char* text, uint64_t n) {
-  {
-    // size the ID table from the line count (about one new ID per line)
-    uint64_t lines = 0;
-    for (const char* q = text; (q = static_cast<const char*>(memchr(q, '\n', text + n - q)));
-         ++q)
-      ++lines;
-    M.ids.reserve(lines / 2 + 16);
-    M.feats.reserve(lines / 2 + 16);
+// Stable byte storage for lines / IDs the parser has to rewrite.
+struct Arena {
+  std::vector<std::unique_ptr<char[]>> blocks;
+  char* cur = nullptr;
+  size_t left = 0;
+  char* alloc(size_t n) {
+    if (n > left) {
+      const size_t sz = std::max<size_t>(n, 1 << 16);
+      blocks.emplace_back(new char[sz]);
+      cur = blocks.back().get();
+      left = sz;
+    }
+    char* p = cur;
+    cur += n;
+    left -= n;
+    return p;
   }
-  int version = 0;  // 0 = auto
+  sv join(std::initializer_list<sv> parts) {
+    size_t n = 0;
+    for (sv p : parts) n += p.size();
+    char* out = alloc(n);
+    char* o = out;
+    for (sv p : parts) {
+      if (!p.empty()) memcpy(o, p.data(), p.size());
+      o += p.size();
+    }
+    return sv(out, n);
+  }
+};
+
+// Settings read_gff fixes on the first accepted line (genome.py:262-292).
+struct GffFormat {
+  int version = 0;  // 0 = auto (no accepted line yet)
   bool have_id_field = true, have_parent_field = true;  // IDfield='ID', parent_field='Parent'
   std::vector<std::string> hierarchy;
-  std::unordered_map<uint32_t, int64_t> renamed;
-  std::string scratch, idbuf;
-  std::vector<sv> words;
+};
+
+// One accepted, non-ignored line after the per-line work that does not touch
+// the model: columns, coordinates, tags, the ID (before de-duplication) and
+// the parent / hierarchy values, each with its hash.
+struct GffLine {
+  sv id, parent, hv[2];
+  uint64_t h_id, h_parent, h_hv[2];
+  // j-th repeat of the previous line's ID (0: differs): the ordered pass
+  // likely renames it to ID2 (j = 1) or ID-(j+1); h_dup is that name's hash
+  uint64_t h_dup;
+  uint32_t dup_run;
+  int64_t lo, hi;
+  uint32_t seqid, ftype, strand;  // chunk-local codes (LocalIntern)
+  uint8_t has_parent, hv_mask;
+};
+
+// Chunk-local string codes (seqid, type, strand) so that the ordered pass
+// maps a few codes per chunk to the model's instead of comparing text.
+struct LocalIntern {
+  std::vector<sv> strs;
+  std::unordered_map<sv, uint32_t> map;
+  uint32_t last = ~0u;
+  uint32_t code(sv s) {
+    if (last != ~0u && strs[last] == s) return last;
+    auto it = map.find(s);
+    if (it == map.end()) {
+      it = map.emplace(s, (uint32_t)strs.size()).first;
+      strs.push_back(s);
+    }
+    return last = it->second;
+  }
+};
+
+// The line's columns (the 8 tabs exactly; '\r' stripped, '\n' ends a line).
+// Returns false for lines read_gff skips.
+inline bool split_line(const char* raw, uint64_t rl, Arena& arena, sv cols[9]) {
+  if (rl == 0 || raw[0] == '#') return false;
+  uint32_t tpos[9];
+  int tabs = 0;
+  bool cr = false;
+  for (uint64_t i = 0; i < rl; ++i) {
+    const char ch = raw[i];
+    if (ch == '\t') {
+      if (tabs < 9) tpos[tabs] = (uint32_t)i;
+      ++tabs;
+    }
+    cr |= ch == '\r';
+  }
+  if (tabs != 8) return false;
+  sv line(raw, rl);
+  if (cr) {  // line.replace('\n', '').replace('\r', '')
+    char* o = arena.alloc(rl);
+    size_t m = 0;
+    for (uint64_t i = 0; i < rl; ++i)
+      if (raw[i] != '\n' && raw[i] != '\r') o[m++] = raw[i];
+    line = sv(o, m);
+    tabs = 0;
+    for (size_t i = 0; i < line.size(); ++i)
+      if (line[i] == '\t') tpos[tabs++] = (uint32_t)i;
+  } else if (raw[rl - 1] == '\n') {
+    line = sv(raw, rl - 1);
+  }
+  size_t b = 0;
+  for (int c = 0; c < 8; ++c) {
+    cols[c] = line.substr(b, tpos[c] - b);
+    b = tpos[c] + 1;
+  }
+  cols[8] = line.substr(b);
+  return true;
+}
+
+// Version / ID-field / hierarchy detection from the first accepted line.
+void detect_format(GffFormat& F, sv tags_text) {
+  if (tags_text.find('=') != sv::npos) {
+    F.version = 3;
+    return;
+  }
+  F.version = 2;
+  std::string spaced = " " + std::string(tags_text);
+  std::replace(spaced.begin(), spaced.end(), ';', ' ');
+  if (F.have_id_field && F.hierarchy.empty() && spaced.find(" ID ") == std::string::npos) {
+    F.have_id_field = false;
+    F.have_parent_field = false;
+    const bool g = tags_text.find("gene_id") != sv::npos;
+    const bool t = tags_text.find("transcript_id") != sv::npos;
+    if (g && t) F.hierarchy = {"transcript_id", "gene_id"};
+    else if (g) F.hierarchy = {"gene_id"};
+  }
+}
+
+// The de-duplicated name of the r-th line (r >= 2) holding an existing ID
+// (genome.py:330-338): ID2, then ID-3, ID-4 ...
+inline void dup_name(sv id, uint32_t j, std::string& out) {
+  out.assign(id.data(), id.size());
+  if (j == 1) {
+    out += '2';
+  } else {
+    out += '-';
+    out += std::to_string(j + 1);
+  }
+}
+
+struct LineParser {
+  const GffFormat& F;
+  Arena arena;
   Tags tags;
-  sv last_seqid, last_strand;
-  uint32_t last_sq = 0, last_st = 0;
-  bool first_line = true;
-  uint64_t pos = 0;
-  while (pos < n) {
-    const char* nl = static_cast<const char*>(memchr(text + pos, '\n', n - pos));
-    const uint64_t end = nl ? (uint64_t)(nl - text) + 1 : n;
-    const char* raw = text + pos;
-    const uint64_t rl = end - pos;
-    pos = end;
-    if (raw[0] == '#') continue;
-    // the 8 tabs (exactly) of an accepted line
-    uint32_t tpos[9];
-    int tabs = 0;
-    bool cr = false;
-    for (uint64_t i = 0; i < rl; ++i) {
-      const char ch = raw[i];
-      if (ch == '\t') {
-        if (tabs < 9) tpos[tabs] = (uint32_t)i;
-        ++tabs;
-      }
-      cr |= ch == '\r';
-    }
-    if (tabs != 8) continue;
-    // line.replace('\n', '').replace('\r', '')  ('\n' only ends a line)
-    sv line(raw, rl);
-    if (cr) {
-      scratch.clear();
-      for (uint64_t i = 0; i < rl; ++i)
-        if (raw[i] != '\n' && raw[i] != '\r') scratch.push_back(raw[i]);
-      line = sv(scratch);
-      tabs = 0;
-      for (size_t i = 0; i < line.size(); ++i)
-        if (line[i] == '\t') tpos[tabs++] = (uint32_t)i;
-    } else if (rl && raw[rl - 1] == '\n') {
-      line = sv(raw, rl - 1);
-    }
+  std::vector<sv> words;
+  LocalIntern seqids, ftypes, strands;
+  sv prev_id;
+  uint32_t prev_run = 0;
+  std::string dup;
+
+  // false: the line is skipped; throws Unsupported on a diagnostic path
+  bool parse(const char* raw, uint64_t rl, GffLine& L) {
     sv cols[9];
-    {
-      size_t b = 0;
-      for (int c = 0; c < 8; ++c) {
-        cols[c] = line.substr(b, tpos[c] - b);
-        b = tpos[c] + 1;
-      }
-      cols[8] = line.substr(b);
-    }
+    if (!split_line(raw, rl, arena, cols)) return false;
     const sv tags_text = cols[8];
-    if (version == 0) {
-      if (tags_text.find('=') != sv::npos) {
-        version = 3;
-      } else {
-        version = 2;
-        std::string spaced = " " + std::string(tags_text);
-        std::replace(spaced.begin(), spaced.end(), ';', ' ');
-        if (have_id_field && hierarchy.empty() && spaced.find(" ID ") == std::string::npos) {
-          have_id_field = false;
-          have_parent_field = false;
-          const bool g = tags_text.find("gene_id") != sv::npos;
-          const bool t = tags_text.find("transcript_id") != sv::npos;
-          if (g && t) hierarchy = {"transcript_id", "gene_id"};
-          else if (g) hierarchy = {"gene_id"};
-        }
-      }
-    }
-    const sv seqid = cols[0];
     const sv ftype = cols[2];
-    if (ftype == "exon") continue;  // features_to_ignore default
+    if (ftype == "exon") return false;  // features_to_ignore default
     int64_t lo = parse_int(cols[3]), hi = parse_int(cols[4]);
     if (lo > hi) std::swap(lo, hi);
-    const sv strand = cols[6];
+    L.lo = lo;
+    L.hi = hi;
+    L.seqid = seqids.code(cols[0]);
+    L.ftype = ftypes.code(ftype);
+    L.strand = strands.code(cols[6]);
     tags.kv.clear();
-    {
-      size_t b = 0;
-      for (;;) {
-        const size_t e = tags_text.find(';', b);
-        const sv item = tags_text.substr(b, e == sv::npos ? sv::npos : e - b);
-        if (!item.empty()) {
-          if (version == 2) {
-            split_ws(item, words);
-            if (words.empty()) throw Unsupported();  // IndexError
-            const size_t q = item.find('"');
-            if (q != sv::npos) {
-              const size_t q2 = item.find('"', q + 1);
-              tags.set(words[0], item.substr(q + 1, q2 == sv::npos ? sv::npos : q2 - q - 1));
-            } else if (words.size() > 1) {
-              tags.set(words[0], words[1]);
-            } else {
-              throw Unsupported();  // print(item); return None
-            }
+    size_t b = 0;
+    for (;;) {
+      const size_t e = tags_text.find(';', b);
+      const sv item = tags_text.substr(b, e == sv::npos ? sv::npos : e - b);
+      if (!item.empty()) {
+        if (F.version == 2) {
+          split_ws(item, words);
+          if (words.empty()) throw Unsupported();  // IndexError
+          const size_t q = item.find('"');
+          if (q != sv::npos) {
+            const size_t q2 = item.find('"', q + 1);
+            tags.set(words[0], item.substr(q + 1, q2 == sv::npos ? sv::npos : q2 - q - 1));
+          } else if (words.size() > 1) {
+            tags.set(words[0], words[1]);
           } else {
-            const size_t q = item.find('=');
-            if (q == sv::npos) throw Unsupported();  // IndexError
-            const size_t q2 = item.find('=', q + 1);
-            tags.set(item.substr(0, q), item.substr(q + 1, q2 == sv::npos ? sv::npos : q2 - q - 1));
+            throw Unsupported();  // print(item); return None
           }
+        } else {
+          const size_t q = item.find('=');
+          if (q == sv::npos) throw Unsupported();  // IndexError
+          const size_t q2 = item.find('=', q + 1);
+          tags.set(item.substr(0, q), item.substr(q + 1, q2 == sv::npos ? sv::npos : q2 - q - 1));
         }
-        if (e == sv::npos) break;
-        b = e + 1;
       }
+      if (e == sv::npos) break;
+      b = e + 1;
     }
     const sv* parent = nullptr;
-    if (have_parent_field) {
+    if (F.have_parent_field) {
       parent = tags.get("Parent");
     } else {
-      for (const std::string& k : hierarchy)
+      for (const std::string& k : F.hierarchy)
         if ((parent = tags.get(k))) break;
     }
-    sv ID;
-    if (have_id_field && tags.get("ID")) {
-      ID = *tags.get("ID");
-    } else if (have_id_field && !parent) {
-      throw Unsupported();  // ID None
-    } else if (parent) {
-      idbuf.assign(parent->data(), parent->size());
-      idbuf += '-';
-      idbuf.append(ftype.data(), ftype.size());
-      ID = idbuf;
-    } else {
-      idbuf.assign(seqid.data(), seqid.size());
-      idbuf += '-';
-      idbuf.append(ftype.data(), ftype.size());
-      idbuf.append(cols[3].data(), cols[3].size());
-      ID = idbuf;
+    const sv* id = F.have_id_field ? tags.get("ID") : nullptr;
+    if (id) L.id = *id;
+    else if (F.have_id_field && !parent) throw Unsupported();  // ID None
+    else if (parent) L.id = arena.join({*parent, "-", ftype});
+    else L.id = arena.join({cols[0], "-", ftype, cols[3]});
+    L.h_id = hash_sv(L.id);
+    L.dup_run = L.id == prev_id ? prev_run + 1 : 0;
+    prev_id = L.id;
+    prev_run = L.dup_run;
+    if (L.dup_run) {
+      dup_name(L.id, L.dup_run, dup);
+      L.h_dup = hash_sv(dup);
     }
-    // de-duplicate against every table; the new name is not re-checked
-    uint32_t idk;
-    {
-      const int64_t k0 = M.ids.find(ID);
-      if (k0 >= 0 && M.lookup((uint32_t)k0) >= 0) {
-        auto it = renamed.find((uint32_t)k0);
-        std::string nid(ID);
-        if (it != renamed.end()) {
-          it->second += 1;
-          nid += "-" + std::to_string(it->second);
-        } else {
-          renamed.emplace((uint32_t)k0, 2);
-          nid += "2";
-        }
-        idk = M.id(nid);
-      } else {
-        idk = M.id(ID);
-      }
-    }
-    // consecutive lines nearly always share seqid and strand
-    if (first_line || seqid != last_seqid) {
-      last_sq = M.seqids.intern(seqid);
-      last_seqid = M.seqids.strs[last_sq];
-    }
-    if (first_line || strand != last_strand) {
-      last_st = M.strands.intern(strand);
-      last_strand = M.strands.strs[last_st];
-    }
-    first_line = false;
-    const uint32_t sq = last_sq, st = last_st;
+    L.has_parent = parent != nullptr;
+    L.hv_mask = 0;
     if (parent) {
-      uint32_t child = idk;
-      for (size_t level = 0; level < hierarchy.size(); ++level) {
-        const sv* pid = tags.get(hierarchy[level]);
-        if (!pid) continue;
-        const std::string& hk = hierarchy[level];
-        const uint32_t t = M.table(sv(hk).substr(0, hk.find('_')));
-        const uint32_t pk = M.id(*pid);
-        const int64_t have = M.slot(t, pk);
-        if (have >= 0) {
-          auto& ch = M.feats[(size_t)have].children;
-          if (std::find(ch.begin(), ch.end(), child) == ch.end()) ch.push_back(child);
-        } else {
-          Feature f;
-          f.type = t;
-          f.seqid = sq;
-          f.strand = st;
-          f.base = false;
-          f.children.push_back(child);
-          M.feats.push_back(std::move(f));
-          M.put(t, pk, (uint32_t)M.feats.size() - 1);
+      L.parent = *parent;
+      L.h_parent = hash_sv(L.parent);
+      for (size_t level = 0; level < F.hierarchy.size(); ++level)
+        if (const sv* pid = tags.get(F.hierarchy[level])) {
+          L.hv[level] = *pid;
+          L.h_hv[level] = hash_sv(*pid);
+          L.hv_mask |= (uint8_t)(1u << level);
         }
-        child = pk;
-      }
-      const int64_t h = M.lookup(*parent);
-      if (h < 0) throw Unsupported();                    // orphan: print, return None
-      Feature& holder = M.feats[(size_t)h];
-      if (holder.base) throw Unsupported();              // BaseAnnotation has no child_list
-      if (std::find(holder.children.begin(), holder.children.end(), idk) == holder.children.end())
-        holder.children.push_back(idk);
     }
-    Feature f;
-    f.type = M.table(ftype);
-    f.seqid = sq;
-    f.lo = lo;
-    f.hi = hi;
-    f.strand = st;
-    f.base = ftype == "CDS" || ftype == "match_part" || ftype == "similarity" || ftype == "region";
-    M.feats.push_back(std::move(f));
-    M.put(M.feats.back().type, idk, (uint32_t)M.feats.size() - 1);
+    return true;
+  }
+};
+
+// read_gff in two passes: the per-line work (columns, tags, IDs, hashes) in
+// parallel over newline-aligned chunks of the text, then the model updates
+// (de-duplication, tables, parents) in file order.  Any diagnostic path
+// anywhere declines the whole input, so chunks may find them out of order.
+void read_gff(Model& M, const char* text, uint64_t n) {
+  const auto t_start = std::chrono::steady_clock::now();
+  GffFormat F;
+  {  // the first accepted line fixes the format
+    Arena arena;
+    sv cols[9];
+    for (uint64_t pos = 0; pos < n;) {
+      const char* nl = static_cast<const char*>(memchr(text + pos, '\n', n - pos));
+      const uint64_t end = nl ? (uint64_t)(nl - text) + 1 : n;
+      const bool ok = split_line(text + pos, end - pos, arena, cols);
+      pos = end;
+      if (ok) {
+        detect_format(F, cols[8]);
+        break;
+      }
+    }
+  }
+  if (F.version == 0) return;
+  // chunks split at line starts
+  unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  if (const char* e = std::getenv("MAGOT_GFF_THREADS")) hw = std::max(1, atoi(e));
+  uint64_t n_chunks = n < (1u << 20) ? 1 : std::min<uint64_t>(hw * 8ull, n >> 16);
+  if (const char* e = std::getenv("MAGOT_GFF_CHUNKS"))  // test hook: force the split
+    n_chunks = std::max<uint64_t>(1, std::min<uint64_t>(strtoull(e, nullptr, 10), n));
+  std::vector<uint64_t> cut(n_chunks + 1, n);
+  cut[0] = 0;
+  for (uint64_t c = 1; c < n_chunks; ++c) {
+    uint64_t p = std::max(cut[c - 1], n * c / n_chunks);
+    const char* nl = p ? static_cast<const char*>(memchr(text + p - 1, '\n', n - p + 1)) : text;
+    cut[c] = !nl ? n : (p ? (uint64_t)(nl - text) + 1 : 0);
+  }
+  std::vector<std::vector<GffLine>> lines(n_chunks);
+  std::vector<std::unique_ptr<LineParser>> parsers(n_chunks);
+  FirstError failed;
+  std::atomic<bool> unsupported{false};
+  std::atomic<uint64_t> next{0};
+  auto work = [&]() {
+    for (uint64_t c; (c = next.fetch_add(1)) < n_chunks && !unsupported.load();) {
+      parsers[c].reset(new LineParser{F, {}, {}, {}});
+      LineParser& P = *parsers[c];
+      std::vector<GffLine>& out = lines[c];
+      out.reserve((cut[c + 1] - cut[c]) / 96 + 16);
+      try {
+        GffLine L;
+        for (uint64_t pos = cut[c]; pos < cut[c + 1];) {
+          const char* nl =
+              static_cast<const char*>(memchr(text + pos, '\n', cut[c + 1] - pos));
+          const uint64_t end = nl ? (uint64_t)(nl - text) + 1 : cut[c + 1];
+          if (P.parse(text + pos, end - pos, L)) out.push_back(L);
+          pos = end;
+        }
+      } catch (const Unsupported&) {
+        unsupported = true;
+      } catch (...) {
+        failed.set();
+        unsupported = true;
+      }
+    }
+  };
+  {
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < std::min<uint64_t>(hw, n_chunks); ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  }
+  failed.rethrow();
+  if (unsupported) throw Unsupported();
+  if (std::getenv("MAGOT_GFF_TIMING"))
+    fprintf(stderr, "[gffplan] parse pass %.3f s (%llu chunks)\n",
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
+            (unsigned long long)n_chunks);
+  uint64_t total = 0;
+  for (auto& v : lines) total += v.size();
+  M.ids.reserve(total + 16);
+  M.feats.reserve(total + 16);
+  M.id_types.reserve(total + 16);
+  M.first_table.reserve(total + 16);
+  M.first_feat.reserve(total + 16);
+
+  // model updates in file order
+  std::vector<uint32_t> renamed;  // per ID: 0, or the last suffix used
+  std::string nid;
+  std::vector<uint32_t> hier_table;
+  for (const std::string& hk : F.hierarchy)
+    hier_table.push_back(M.table(sv(hk).substr(0, hk.find('_'))));
+  std::vector<uint32_t> sq_of, st_of, ty_of;  // chunk code -> model index
+  std::vector<uint8_t> ty_base;
+  constexpr size_t kAhead = 16;
+  sv last_id, last_parent;
+  int64_t last_k0 = -1, last_pk = -1;
+  for (uint64_t c = 0; c < n_chunks; ++c) {
+    const std::vector<GffLine>& V = lines[c];
+    const LineParser& P = *parsers[c];
+    sq_of.assign(P.seqids.strs.size(), ~0u);
+    st_of.assign(P.strands.strs.size(), ~0u);
+    ty_of.assign(P.ftypes.strs.size(), ~0u);
+    ty_base.assign(P.ftypes.strs.size(), 0);
+    for (size_t li = 0; li < V.size(); ++li) {
+      if (li + kAhead < V.size()) {
+        const GffLine& A = V[li + kAhead];
+        M.ids.prefetch(A.dup_run ? A.h_dup : A.h_id);
+        if (A.has_parent) M.ids.prefetch(A.h_parent);
+      }
+      const GffLine& L = V[li];
+      // de-duplicate against every table; the new name is not re-checked
+      uint32_t idk;
+      {
+        // runs of lines share an ID (CDS parts) or a parent: IDs are never
+        // removed, so the last string's index stays valid
+        int64_t k0;
+        if (L.id == last_id) {
+          k0 = last_k0;
+        } else {
+          k0 = M.ids.find(L.id, L.h_id);
+        }
+        if (k0 >= 0 && M.lookup((uint32_t)k0) >= 0) {
+          if (renamed.size() <= (size_t)k0) renamed.resize(M.ids.strs.size() + 1, 0);
+          uint32_t& r = renamed[(size_t)k0];
+          r = r ? r + 1 : 2;
+          dup_name(L.id, r - 1, nid);
+          idk = L.dup_run == r - 1 ? M.id(nid, L.h_dup) : M.id(nid);
+        } else {
+          idk = M.id(L.id, L.h_id);
+          k0 = idk;
+        }
+        last_id = L.id;
+        last_k0 = k0;
+      }
+      // seqids / strands interned in first-seen order, as the Python strings are
+      if (sq_of[L.seqid] == ~0u) sq_of[L.seqid] = M.seqids.intern(P.seqids.strs[L.seqid]);
+      if (st_of[L.strand] == ~0u) st_of[L.strand] = M.strands.intern(P.strands.strs[L.strand]);
+      const uint32_t sq = sq_of[L.seqid], st = st_of[L.strand];
+      if (L.has_parent) {
+        uint32_t child = idk;
+        for (size_t level = 0; level < F.hierarchy.size(); ++level) {
+          if (!((L.hv_mask >> level) & 1)) continue;
+          const uint32_t t = hier_table[level];
+          const uint32_t pk = M.id(L.hv[level], L.h_hv[level]);
+          const int64_t have = M.slot(t, pk);
+          if (have >= 0) {
+            auto& ch = M.feats[(size_t)have].children;
+            if (std::find(ch.begin(), ch.end(), child) == ch.end()) ch.push_back(child);
+          } else {
+            Feature f;
+            f.type = t;
+            f.seqid = sq;
+            f.strand = st;
+            f.base = false;
+            f.children.push_back(child);
+            M.feats.push_back(std::move(f));
+            M.put(t, pk, (uint32_t)M.feats.size() - 1);
+          }
+          child = pk;
+        }
+        if (L.parent != last_parent) {
+          last_pk = M.ids.find(L.parent, L.h_parent);
+          last_parent = L.parent;
+        }
+        const int64_t pk = last_pk;
+        const int64_t h = pk < 0 ? -1 : M.lookup((uint32_t)pk);
+        if (h < 0) throw Unsupported();        // orphan: print, return None
+        Feature& holder = M.feats[(size_t)h];
+        if (holder.base) throw Unsupported();  // BaseAnnotation has no child_list
+        if (std::find(holder.children.begin(), holder.children.end(), idk) ==
+            holder.children.end())
+          holder.children.push_back(idk);
+      }
+      if (ty_of[L.ftype] == ~0u) {  // the table is created at the type's first line
+        const sv ft = P.ftypes.strs[L.ftype];
+        ty_of[L.ftype] = M.table(ft);
+        ty_base[L.ftype] = ft == "CDS" || ft == "match_part" || ft == "similarity" || ft == "region";
+      }
+      Feature f;
+      f.type = ty_of[L.ftype];
+      f.seqid = sq;
+      f.lo = L.lo;
+      f.hi = L.hi;
+      f.strand = st;
+      f.base = ty_base[L.ftype];
+      const uint32_t ty = f.type;
+      M.feats.push_back(std::move(f));
+      M.put(ty, idk, (uint32_t)M.feats.size() - 1);
+    }
   }
 }
 
@@ -553,18 +772,23 @@ std::vector<uint32_t> py2_dict_order(const std::vector<uint32_t>& keys,
 // get_fasta lowering + C ABI
 // ---------------------------------------------------------------------------
 
-struct magot_gffplan {
-  magot::Model model;
-  // interval / record tables for magot_plan_create
+namespace magot {
+// Lowered output: interval / record tables for magot_plan_create and the
+// text skeleton (pieces are text slices or record payload slots).
+struct Piece {
+  uint64_t off, len;  // text piece, or ...
+  int64_t rec;        // ... record payload index (>= 0)
+};
+struct Lowered {
   std::vector<magot_exon> exons;
   std::vector<magot_tx> txs;
-  // skeleton: text pieces (offset/length into `text`) and record slots
   std::string text;
-  struct Piece {
-    uint64_t off, len;  // text piece, or ...
-    int64_t rec;        // ... record payload index (>= 0)
-  };
   std::vector<Piece> pieces;
+};
+}  // namespace magot
+
+struct magot_gffplan : magot::Lowered {
+  magot::Model model;
   bool protein = false;
 };
 
@@ -572,14 +796,23 @@ namespace magot {
 namespace {
 
 struct Lowering {
-  magot_gffplan& P;
-  const std::unordered_map<std::string, uint32_t>& contig_of;
+  Lowered& P;
+  const Model& M;
+  const bool protein;
+  const std::vector<int64_t>& contig_idx;  // seqid -> contig (-1: missing)
   const uint64_t* contig_len;
+  const std::vector<uint32_t>& id_of_feat;  // the ID a feature was stored under
 
-  void text(const std::string& s) {
+  void text(sv s) {
     if (s.empty()) return;
     P.pieces.push_back({P.text.size(), s.size(), -1});
     P.text += s;
+  }
+  void header(sv id) {  // ">" + ID + "\n"
+    P.pieces.push_back({P.text.size(), id.size() + 2, -1});
+    P.text += '>';
+    P.text += id;
+    P.text += '\n';
   }
 
   // slice contig[a:b] (Python rules, step 1) -> (start, length)
@@ -601,7 +834,6 @@ struct Lowering {
   // ParentAnnotation.get_fasta (genome.py:677-731), longest=False, genomic=False.
   // Returns the number of records emitted ("" <=> 0).
   uint64_t fasta(uint32_t fi, bool first_in_join) {
-    const Model& M = P.model;
     const Feature& F = M.feats[fi];
     if (F.children.empty()) return 0;
     const int64_t first = M.lookup(F.children[0]);
@@ -618,12 +850,7 @@ struct Lowering {
         if (!C.base) throw Unsupported();  // mixed children: print
         const sv sd = M.strands.strs[C.strand];
         if (sd != "+" && sd != "." && sd != "-") throw Unsupported();  // invalid strand: print
-        if (contig_idx.size() < M.seqids.strs.size()) contig_idx.resize(M.seqids.strs.size(), -2);
-        int64_t& cix = contig_idx[C.seqid];
-        if (cix == -2) {
-          auto ci = contig_of.find(std::string(M.seqids.strs[C.seqid]));
-          cix = ci == contig_of.end() ? -1 : (int64_t)ci->second;
-        }
+        const int64_t cix = contig_idx[C.seqid];
         if (cix < 0) throw Unsupported();  // missing seqid: print
         magot_exon x;
         uint64_t st, ln;
@@ -648,9 +875,9 @@ struct Lowering {
       if (M.strands.strs[strand] == "-") std::reverse(by.begin(), by.end());
       uint64_t total = 0;
       for (auto& e : by) total += e.second.len;
-      if (P.protein && total <= 2) throw Unsupported();  // translate() -> None
+      if (protein && total <= 2) throw Unsupported();  // translate() -> None
       if (!first_in_join) text("\n");
-      text(">" + std::string(M.ids.strs[idk_of(fi)]) + "\n");
+      header(M.ids.strs[id_of_feat[fi]]);
       magot_tx t;
       t.exon_begin = P.exons.size();
       t.n_exons = (uint32_t)by.size();
@@ -670,11 +897,23 @@ struct Lowering {
     return n;
   }
 
-  // the ID a feature was stored under (ParentAnnotation.ID)
-  std::vector<uint32_t> id_of_feat;
-  std::vector<int64_t> contig_idx;  // seqid -> contig (-1 missing, -2 unknown yet)
-  uint32_t idk_of(uint32_t fi) const { return id_of_feat[fi]; }
 };
+
+// Appends `part` (lowered from a later run of keys) to `all`.
+void append_lowered(Lowered& all, const Lowered& part) {
+  const uint64_t x0 = all.exons.size(), t0 = all.txs.size(), c0 = all.text.size();
+  all.exons.insert(all.exons.end(), part.exons.begin(), part.exons.end());
+  for (magot_tx t : part.txs) {
+    t.exon_begin += x0;
+    all.txs.push_back(t);
+  }
+  all.text += part.text;
+  for (Piece pc : part.pieces) {
+    if (pc.rec < 0) pc.off += c0;
+    else pc.rec += (int64_t)t0;
+    all.pieces.push_back(pc);
+  }
+}
 
 }  // namespace
 }  // namespace magot
@@ -709,10 +948,14 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
     magot::Model& M = P->model;
     std::unordered_map<std::string, uint32_t> contig_of;
     for (uint32_t i = 0; i < n_contigs; ++i) contig_of[seqids[i]] = i;  // last duplicate wins
-    magot::Lowering L{*P, contig_of, contig_lens, {}, {}};
-    L.id_of_feat.assign(M.feats.size(), 0);
+    std::vector<int64_t> contig_idx(M.seqids.strs.size(), -1);
+    for (size_t q = 0; q < contig_idx.size(); ++q) {
+      auto ci = contig_of.find(std::string(M.seqids.strs[q]));
+      if (ci != contig_of.end()) contig_idx[q] = ci->second;
+    }
+    std::vector<uint32_t> id_of_feat(M.feats.size(), 0);
     for (uint32_t ti2 = 0; ti2 < M.tables.size(); ++ti2)
-      for (uint32_t k : M.tables[ti2].keys) L.id_of_feat[(size_t)M.slot(ti2, k)] = k;
+      for (uint32_t k : M.tables[ti2].keys) id_of_feat[(size_t)M.slot(ti2, k)] = k;
     auto ti = M.table_index.find(feature);
     if (ti == M.table_index.end()) throw Unsupported();  // AttributeError
     const magot::Table& T = M.tables[ti->second];
@@ -725,12 +968,48 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
     }
     lap("order");
     // "\n".join(obj.get_fasta() for obj in table.values()): every object adds
-    // its records (a blank line when it has none)
-    for (size_t i = 0; i < keys.size(); ++i) {
-      const uint32_t fi = (uint32_t)M.slot(ti->second, keys[i]);
-      if (M.feats[fi].base) throw Unsupported();  // BaseAnnotation has no get_fasta
-      if (i) L.text("\n");
-      L.fasta(fi, true);
+    // its records (a blank line when it has none).  The model is read-only
+    // here, so runs of keys are lowered in parallel and appended in order.
+    const uint32_t table = ti->second;
+    const size_t n_keys = keys.size();
+    size_t n_parts = n_keys < 4096 ? 1 : std::min<size_t>(64, n_keys / 2048);
+    if (const char* e = std::getenv("MAGOT_GFF_CHUNKS"))  // test hook: force the split
+      n_parts = std::max<size_t>(1, std::min<size_t>(strtoull(e, nullptr, 10), n_keys));
+    std::vector<magot::Lowered> parts(n_parts);
+    magot::FirstError failed;
+    std::atomic<bool> unsupported{false};
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t q; (q = next.fetch_add(1)) < n_parts && !unsupported.load();) {
+        magot::Lowered& out = q ? parts[q] : *P;
+        magot::Lowering L{out, M, P->protein, contig_idx, contig_lens, id_of_feat};
+        try {
+          for (size_t i = n_keys * q / n_parts; i < n_keys * (q + 1) / n_parts; ++i) {
+            const uint32_t fi = (uint32_t)M.slot(table, keys[i]);
+            if (M.feats[fi].base) throw Unsupported();  // BaseAnnotation has no get_fasta
+            if (i) L.text("\n");
+            L.fasta(fi, true);
+          }
+        } catch (const Unsupported&) {
+          unsupported = true;
+        } catch (...) {
+          failed.set();
+          unsupported = true;
+        }
+      }
+    };
+    {
+      const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+      std::vector<std::thread> pool;
+      for (unsigned t = 1; t < std::min<size_t>(hw, n_parts); ++t) pool.emplace_back(work);
+      work();
+      for (auto& t : pool) t.join();
+    }
+    failed.rethrow();
+    if (unsupported) throw Unsupported();
+    for (size_t q = 1; q < n_parts; ++q) {
+      magot::append_lowered(*P, parts[q]);
+      parts[q] = magot::Lowered();
     }
     lap("lower");
   } catch (const Unsupported&) {

@@ -150,3 +150,60 @@ def test_native_plan_dedupe_and_join_shapes():
             got = native_gff2fasta(fasta, gff, seq_type, order)
             assert got is not None
             assert got == mo.gff2fasta(fasta, gff, seq_type=seq_type, order=order)
+
+
+def _dup_heavy_gff():
+    """Shared CDS IDs in runs, an ID repeated out of run order, CRLF lines,
+    comments and ignored exons: the ordered pass's rename prediction and the
+    chunk split both have to hold."""
+    rows = []
+    for g in range(40):
+        lo = 1 + 30 * (g % 9)
+        rows.append('c1\tx\tgene\t%d\t%d\t.\t%s\t.\tID=g%d' % (lo, lo + 25, '+-'[g % 2], g))
+        rows.append('c1\tx\tmRNA\t%d\t%d\t.\t%s\t.\tID=m%d;Parent=g%d' % (lo, lo + 25, '+-'[g % 2], g, g))
+        if g % 5 == 0:
+            rows.append('# a comment line')
+        for k in range(1 + g % 4):
+            rows.append('c1\tx\texon\t%d\t%d\t.\t+\t.\tID=e%d;Parent=m%d' % (lo + k, lo + k + 4, g, g))
+            cid = 'shared' if g % 7 == 3 else 'cds%d' % (g // 2)
+            rows.append('c1\tx\tCDS\t%d\t%d\t.\t%s\t0\tID=%s;Parent=m%d'
+                        % (lo + 5 * k, lo + 5 * k + 4, '+-'[g % 2], cid, g))
+    text = ''
+    for i, r in enumerate(rows):
+        text += r + ('\r\n' if i % 11 == 0 else '\n')
+    return text
+
+
+@pytest.mark.parametrize('chunks', [1, 2, 7, 64])
+def test_native_plan_chunked_parse(monkeypatch, chunks):
+    """The parallel parse and lowering passes over forced splits give the oracle's
+    output (renamed IDs across chunk boundaries included)."""
+    monkeypatch.setenv('MAGOT_GFF_CHUNKS', str(chunks))
+    fasta = '>c1\n' + 'ACGTTGCAACGGAT' * 30 + '\n'
+    gff = _dup_heavy_gff()
+    for seq_type in ('nucleotide', 'protein'):
+        for order in ('insertion', 'py2'):
+            got = native_gff2fasta(fasta, gff, seq_type, order)
+            assert got is not None
+            assert got == mo.gff2fasta(fasta, gff, seq_type=seq_type, order=order)
+
+
+@pytest.mark.parametrize('fmt', ['gff3', 'gtf'])
+def test_native_plan_chunked_synthetic(monkeypatch, fmt):
+    monkeypatch.setenv('MAGOT_GFF_CHUNKS', '13')
+    w = synth.make('small', seed=5, genome_bases=300_000, n_tx=200, iupac_rate=1e-3)
+    fasta = w.fasta_text()
+    gff = w.gff3_text() if fmt == 'gff3' else w.gtf_text()
+    got = native_gff2fasta(fasta, gff, 'protein', 'py2')
+    assert got is not None
+    assert got == mo.gff2fasta(fasta, gff, seq_type='protein', order='py2')
+
+
+def test_native_plan_chunked_declines(monkeypatch):
+    """A diagnostic line found by a later chunk still declines the input."""
+    monkeypatch.setenv('MAGOT_GFF_CHUNKS', '5')
+    gs = G.GenomeSequence('>c1\n' + 'ACGT' * 100 + '\n')
+    good = ''.join('c1\tx\tgene\t1\t9\t.\t+\t.\tID=g%d\n' % i for i in range(50))
+    assert engine.GffPlan.build(good, list(gs), [400], protein=True) is not None
+    bad = good + 'c1\tx\tgene\t1\tten\t.\t+\t.\tID=gz\n'
+    assert engine.GffPlan.build(bad, list(gs), [400], protein=True) is None
