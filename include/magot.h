@@ -271,6 +271,26 @@ int magot_gffplan_render(const magot_gffplan* p, const uint8_t* nuc, const uint6
                          uint64_t* out_len);
 void magot_gffplan_destroy(magot_gffplan* p);
 
+/*
+ * The same FASTA text assembled on device: the skeleton of
+ * `gp` is uploaded once, and each execute fills it with the payloads of
+ * extraction plan `p` (built from gp's tables, with MAGOT_OUT_PEP for a
+ * protein skeleton, MAGOT_OUT_NUC otherwise) in one device buffer: per-unit
+ * lengths (trimX applied), a scan, and a copy kernel.  fetch synchronises and
+ * copies the *out_len bytes (out == NULL: length only).  max_bytes bounds
+ * *out_len.  p must outlive the handle.  Replaces the text building of
+ * AnnotationSet.get_fasta / ParentAnnotation.get_fasta
+ * (genome.py:578-582, 677-731) for the gff2fasta CLI (genome_tools.py:330).
+ */
+typedef struct magot_fasta_text magot_fasta_text;
+int magot_fasta_text_create(magot_ctx* ctx, const magot_gffplan* gp, const magot_plan* p,
+                            magot_fasta_text** out, uint64_t* max_bytes);
+int magot_fasta_text_execute(magot_ctx* ctx, magot_fasta_text* t);
+int magot_fasta_text_fetch(magot_ctx* ctx, magot_fasta_text* t, uint8_t* out, uint64_t cap,
+                           uint64_t* out_len);
+int magot_fasta_text_time(magot_ctx* ctx, magot_fasta_text* t, int iters, double* avg_ms);
+void magot_fasta_text_destroy(magot_fasta_text* t);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,6 +36,8 @@ EXPORTS = (
     'magot_orf6_sizes', 'magot_orf6_batch', 'magot_plan_orf6', 'magot_orf6_execute',
     'magot_orf6_fetch', 'magot_orf6_time', 'magot_orf6_destroy',
     'magot_genome_load_fasta', 'magot_genome_contigs', 'magot_fasta_read',
+    'magot_fasta_text_create', 'magot_fasta_text_execute', 'magot_fasta_text_fetch',
+    'magot_fasta_text_time', 'magot_fasta_text_destroy',
 )
 
 ERR_UNSUPPORTED = -5
@@ -105,6 +107,12 @@ def _declare(lib):
         'magot_orf6_time': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_double)]),
         'magot_orf6_destroy': (None, [_vp]),
+        'magot_fasta_text_create': (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(_vp), _u64p]),
+        'magot_fasta_text_execute': (ctypes.c_int, [_vp, _vp]),
+        'magot_fasta_text_fetch': (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _u64p]),
+        'magot_fasta_text_time': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
+                                                 ctypes.POINTER(ctypes.c_double)]),
+        'magot_fasta_text_destroy': (None, [_vp]),
         'magot_genome_load_fasta': (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_uint64,
                                                    ctypes.c_int, ctypes.POINTER(_vp)]),
         'magot_genome_contigs': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32), _vp, _vp,

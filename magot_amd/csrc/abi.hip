@@ -1057,3 +1057,151 @@ void magot_orf6_destroy(magot_orf6* o) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// FASTA text assembly on device (render.hip)
+// ---------------------------------------------------------------------------
+
+struct magot_fasta_text {
+  magot_ctx* ctx = nullptr;
+  const magot_plan* plan = nullptr;
+  void* arena = nullptr;
+  const TextUnit* units = nullptr;
+  const uint64_t* roff = nullptr;
+  const uint8_t* text = nullptr;
+  uint64_t* len = nullptr;
+  uint64_t* end = nullptr;
+  void* scan_tmp = nullptr;
+  size_t scan_bytes = 0;
+  uint8_t* out = nullptr;
+  uint64_t n_units = 0, cap = 0;
+  int protein = 0;
+  void launch(hipStream_t s) const {
+    launch_text_assembly(units, n_units, roff, protein ? plan->args.pep : plan->args.nuc,
+                         protein, text, len, end, scan_tmp, scan_bytes, out, s);
+  }
+};
+
+extern "C" {
+
+int magot_fasta_text_create(magot_ctx* ctx, const magot_gffplan* gp, const magot_plan* p,
+                            magot_fasta_text** out, uint64_t* max_bytes) {
+  if (int rc = bind(ctx)) return rc;
+  if (!gp || !p || !out) {
+    set_error("magot_fasta_text_create: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  const std::string* text = nullptr;
+  std::vector<TextUnit> units;
+  bool protein = false;
+  uint64_t n_rec = 0;
+  if (!gffplan_units(gp, &text, &units, &protein, &n_rec)) {
+    set_error("magot_fasta_text_create: too many records");
+    return MAGOT_ERR_ARG;
+  }
+  if (n_rec != p->n_tx || !(p->args.outputs & (protein ? MAGOT_OUT_PEP : MAGOT_OUT_NUC))) {
+    set_error("magot_fasta_text_create: the plan was not built from this skeleton's tables");
+    return MAGOT_ERR_ARG;
+  }
+  std::unique_ptr<magot_fasta_text> o(new magot_fasta_text());
+  o->ctx = ctx;
+  o->plan = p;
+  o->protein = protein;
+  o->n_units = units.size();
+  const std::vector<uint64_t>& roff = protein ? p->pep_off : p->nuc_off;
+  o->cap = text->size() + (roff.empty() ? 0 : roff.back());
+  o->scan_bytes = text_scan_bytes(o->n_units);
+  Carve cv;
+  const uint64_t o_units = cv.take<TextUnit>(o->n_units);
+  const uint64_t o_roff = cv.take<uint64_t>(roff.size());
+  const uint64_t o_text = cv.take<uint8_t>(text->size());
+  const uint64_t o_len = cv.take<uint64_t>(o->n_units);
+  const uint64_t o_end = cv.take<uint64_t>(o->n_units);
+  const uint64_t o_tmp = cv.take<uint8_t>(o->scan_bytes);
+  const uint64_t o_out = cv.take<uint8_t>(o->cap);
+  MAGOT_HIP_TRY(hipMalloc(&o->arena, cv.used));
+  char* base = static_cast<char*>(o->arena);
+  o->units = reinterpret_cast<const TextUnit*>(base + o_units);
+  o->roff = reinterpret_cast<const uint64_t*>(base + o_roff);
+  o->text = reinterpret_cast<const uint8_t*>(base + o_text);
+  o->len = reinterpret_cast<uint64_t*>(base + o_len);
+  o->end = reinterpret_cast<uint64_t*>(base + o_end);
+  o->scan_tmp = base + o_tmp;
+  o->out = reinterpret_cast<uint8_t*>(base + o_out);
+  if (!units.empty())
+    MAGOT_HIP_TRY(hipMemcpy(base + o_units, units.data(), units.size() * sizeof(TextUnit),
+                            hipMemcpyHostToDevice));
+  if (!roff.empty())
+    MAGOT_HIP_TRY(hipMemcpy(base + o_roff, roff.data(), roff.size() * 8, hipMemcpyHostToDevice));
+  if (!text->empty())
+    MAGOT_HIP_TRY(hipMemcpy(base + o_text, text->data(), text->size(), hipMemcpyHostToDevice));
+  if (max_bytes) *max_bytes = o->cap;
+  *out = o.release();
+  return MAGOT_OK;
+}
+
+int magot_fasta_text_execute(magot_ctx* ctx, magot_fasta_text* o) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o) {
+    set_error("magot_fasta_text_execute: null handle");
+    return MAGOT_ERR_ARG;
+  }
+  if (!o->plan->executed) {
+    set_error("magot_fasta_text_execute: execute the extraction plan first");
+    return MAGOT_ERR_ARG;
+  }
+  o->launch(ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  return MAGOT_OK;
+}
+
+int magot_fasta_text_fetch(magot_ctx* ctx, magot_fasta_text* o, uint8_t* out, uint64_t cap,
+                           uint64_t* out_len) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o || !out_len) {
+    set_error("magot_fasta_text_fetch: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  uint64_t n = 0;
+  if (o->n_units)
+    MAGOT_HIP_TRY(hipMemcpy(&n, o->end + o->n_units - 1, 8, hipMemcpyDeviceToHost));
+  *out_len = n;
+  if (!out) return MAGOT_OK;
+  if (cap < n) {
+    set_error("magot_fasta_text_fetch: output buffer too small");
+    return MAGOT_ERR_ARG;
+  }
+  if (n) MAGOT_HIP_TRY(hipMemcpy(out, o->out, n, hipMemcpyDeviceToHost));
+  return MAGOT_OK;
+}
+
+int magot_fasta_text_time(magot_ctx* ctx, magot_fasta_text* o, int iters, double* avg_ms) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o || !avg_ms || iters <= 0) {
+    set_error("magot_fasta_text_time: bad argument");
+    return MAGOT_ERR_ARG;
+  }
+  double total = 0;
+  for (int i = 0; i < iters; ++i) {
+    MAGOT_HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    o->launch(ctx->stream);
+    MAGOT_HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    MAGOT_HIP_TRY(hipEventSynchronize(ctx->ev1));
+    float ms = 0;
+    MAGOT_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    total += ms;
+  }
+  *avg_ms = total / iters;
+  return MAGOT_OK;
+}
+
+void magot_fasta_text_destroy(magot_fasta_text* o) {
+  if (!o) return;
+  if (o->ctx) (void)hipSetDevice(o->ctx->device);
+  if (o->arena) (void)hipFree(o->arena);
+  delete o;
+}
+
+}  // extern "C"

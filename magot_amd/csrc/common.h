@@ -127,6 +127,26 @@ void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const 
                       const uint8_t* strands, const uint64_t* pep_off, uint64_t total_pep,
                       const uint32_t* lut16, uint8_t* out, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// FASTA text assembly (render.hip, gffplan.cpp)
+// ---------------------------------------------------------------------------
+// A run of skeleton text followed by at most one record payload.
+constexpr uint32_t kNoRecord = 0xFFFFFFFFu;
+struct TextUnit {
+  uint64_t text_off;
+  uint32_t text_len;
+  uint32_t rec;  // record index, or kNoRecord
+};
+// The planner's skeleton as units (consecutive text pieces merged).
+// Returns false when a record index does not fit a TextUnit.
+bool gffplan_units(const magot_gffplan* p, const std::string** text, std::vector<TextUnit>* units,
+                   bool* protein, uint64_t* n_rec);
+size_t text_scan_bytes(uint64_t n);
+void launch_text_assembly(const TextUnit* units, uint64_t n, const uint64_t* roff,
+                          const uint8_t* pay, int protein, const uint8_t* text, uint64_t* len,
+                          uint64_t* end, void* scan_tmp, size_t scan_bytes, uint8_t* out,
+                          hipStream_t s);
+
 // Standard genetic code (genome.py:795-802) as a 64-byte table indexed
 // c0 + 4*c1 + 16*c2 with A=0, C=1, G=2, T=3.
 void standard_lut(uint8_t out[64]);

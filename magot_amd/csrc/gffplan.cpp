@@ -634,6 +634,7 @@ void read_gff(Model& M, const char* text, uint64_t n) {
       const GffLine& L = V[li];
       // de-duplicate against every table; the new name is not re-checked
       uint32_t idk;
+      const size_t n_ids = M.ids.strs.size();
       {
         // runs of lines share an ID (CDS parts) or a parent: IDs are never
         // removed, so the last string's index stays valid
@@ -691,8 +692,10 @@ void read_gff(Model& M, const char* text, uint64_t n) {
         if (h < 0) throw Unsupported();        // orphan: print, return None
         Feature& holder = M.feats[(size_t)h];
         if (holder.base) throw Unsupported();  // BaseAnnotation has no child_list
-        if (std::find(holder.children.begin(), holder.children.end(), idk) ==
-            holder.children.end())
+        // without a hierarchy, a name interned on this line is in no child list yet
+        if ((idk >= n_ids && F.hierarchy.empty()) ||
+            std::find(holder.children.begin(), holder.children.end(), idk) ==
+                holder.children.end())
           holder.children.push_back(idk);
       }
       if (ty_of[L.ftype] == ~0u) {  // the table is created at the type's first line
@@ -1034,6 +1037,43 @@ int magot_gffplan_tables(const magot_gffplan* p, magot_exon* exons, magot_tx* tx
   if (txs && !p->txs.empty()) memcpy(txs, p->txs.data(), p->txs.size() * sizeof(magot_tx));
   return MAGOT_OK;
 }
+
+}  // extern "C"
+
+namespace magot {
+
+bool gffplan_units(const magot_gffplan* p, const std::string** text, std::vector<TextUnit>* units,
+                   bool* protein, uint64_t* n_rec) {
+  *text = &p->text;
+  *protein = p->protein;
+  *n_rec = p->txs.size();
+  if (p->txs.size() >= kNoRecord) return false;
+  units->clear();
+  TextUnit cur{0, 0, kNoRecord};
+  for (const Piece& pc : p->pieces) {
+    if (pc.rec >= 0) {
+      cur.rec = (uint32_t)pc.rec;
+      units->push_back(cur);
+      cur = TextUnit{0, 0, kNoRecord};
+      continue;
+    }
+    // text pieces are laid out back to back in `text`, so runs merge
+    if (cur.text_len && (cur.text_off + cur.text_len != pc.off ||
+                         cur.text_len + pc.len > 0xFFFFFFFFull)) {
+      units->push_back(cur);
+      cur = TextUnit{0, 0, kNoRecord};
+    }
+    if (pc.len > 0xFFFFFFFFull) return false;
+    if (!cur.text_len) cur.text_off = pc.off;
+    cur.text_len += (uint32_t)pc.len;
+  }
+  if (cur.text_len) units->push_back(cur);
+  return true;
+}
+
+}  // namespace magot
+
+extern "C" {
 
 // Record payload: nucleotide bytes, or the translation with one leading 'X'
 // dropped (trimX, genome.py:819-821).

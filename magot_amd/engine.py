@@ -303,6 +303,55 @@ class GffPlan(object):
             pass
 
 
+class FastaText(object):
+    """The gff2fasta text assembled on device (magot_fasta_text_*): the
+    GffPlan skeleton filled with an ExtractionPlan's payloads in one device
+    buffer, fetched with a single D2H."""
+
+    def __init__(self, gffplan, extraction):
+        L = _lib.lib()
+        self.ctx = extraction.ctx
+        self._keep = (gffplan, extraction)
+        h = ctypes.c_void_p()
+        cap = ctypes.c_uint64()
+        check(L.magot_fasta_text_create(self.ctx.handle, gffplan.handle, extraction.handle,
+                                        ctypes.byref(h), ctypes.byref(cap)),
+              'magot_fasta_text_create')
+        self.handle = h
+        self.max_bytes = cap.value
+
+    def execute(self):
+        check(_lib.lib().magot_fasta_text_execute(self.ctx.handle, self.handle),
+              'magot_fasta_text_execute')
+
+    def fetch(self):
+        """The text as a bytes-like numpy array (no trailing newline)."""
+        L = _lib.lib()
+        out = np.empty(max(self.max_bytes, 1), dtype=np.uint8)
+        n = ctypes.c_uint64()
+        check(L.magot_fasta_text_fetch(self.ctx.handle, self.handle, ptr(out), self.max_bytes,
+                                       ctypes.byref(n)), 'magot_fasta_text_fetch')
+        return out[:n.value]
+
+    def time(self, iters):
+        ms = ctypes.c_double()
+        check(_lib.lib().magot_fasta_text_time(self.ctx.handle, self.handle, int(iters),
+                                               ctypes.byref(ms)), 'magot_fasta_text_time')
+        return ms.value
+
+    def close(self):
+        if getattr(self, 'handle', None):
+            _lib.lib().magot_fasta_text_destroy(self.handle)
+            self.handle = None
+        self._keep = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _concat(seqs):
     parts = [_as_bytes(s) for s in seqs]
     off = np.zeros(len(parts) + 1, dtype=np.uint64)

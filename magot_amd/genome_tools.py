@@ -44,6 +44,17 @@ def _write(text):
         sys.stdout.write(text)
 
 
+def _write_bytes(*parts):
+    out = getattr(sys.stdout, 'buffer', None)
+    if out is not None:
+        sys.stdout.flush()
+        for p in parts:
+            out.write(p)
+        out.flush()
+    else:
+        sys.stdout.write(''.join(bytes(p).decode('latin-1') for p in parts))
+
+
 def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', longest='False',
               genomic='False', order='py2', native='True'):
     """genome_tools.py:324-330.
@@ -56,7 +67,7 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
             _literal(genomic) is False and seq_type in ('nucleotide', 'protein')):
         text = _gff2fasta_native(genome_sequence, gff, seq_type, order)
         if text is not None:
-            _write(text + '\n')
+            _write_bytes(text, b'\n')
             return
     g = genome.Genome(genome_sequence)
     if from_exons == 'True':
@@ -70,7 +81,8 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
 
 
 def _gff2fasta_native(genome_sequence, gff, seq_type, order):
-    """The gff2fasta text via the native planner, or None when it declines."""
+    """The gff2fasta text (bytes) via the native planner, the extraction
+    kernel and device text assembly, or None when the planner declines."""
     if order not in ('py2', 'insertion'):
         raise ValueError("order must be 'insertion' or 'py2'")
     # the FASTA is read and packed natively; Python reader for unusual headers
@@ -87,11 +99,14 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order):
     try:
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                    engine.OUT_PEP if protein else engine.OUT_NUC)
+        text = engine.FastaText(plan, ex)
         try:
-            nuc, noff, pep, poff = ex.run()
+            ex.execute()
+            text.execute()  # records + headers + joiners in one device buffer
+            return text.fetch()
         finally:
+            text.close()
             ex.close()
-        return plan.render(nuc, noff, pep, poff).decode('latin-1')
     finally:
         plan.close()
 

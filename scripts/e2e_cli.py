@@ -1,7 +1,7 @@
 """End-to-end gff2fasta on a BASELINE-shaped synthetic (default C3): writes the
 FASTA + GFF3 text files, then times each phase of the native CLI path
 (genome_tools._gff2fasta_native) -- FASTA parse, native GFF plan, genome pack
-+ H2D, plan upload, kernel, D2H, text render -- and checks the output
++ H2D, plan upload, kernel, device text assembly, one D2H -- and checks the output
 against the C oracle's record bytes.  Writes one JSON line.
 
     python scripts/e2e_cli.py [--config C3] [--seq-type protein] [--dir /tmp/magot_e2e]
@@ -56,11 +56,15 @@ def main():
     ex.sync()
     ph['kernel'] = time.perf_counter() - t
     t = time.perf_counter()
-    nuc, noff, pep, poff = ex.fetch()
-    ph['d2h'] = time.perf_counter() - t
+    ft = engine.FastaText(plan, ex)
+    ph['text_skeleton_h2d'] = time.perf_counter() - t
     t = time.perf_counter()
-    text = plan.render(nuc, noff, pep, poff)
-    ph['render'] = time.perf_counter() - t
+    ft.execute()
+    ex.sync()
+    ph['text_assembly_device'] = time.perf_counter() - t
+    t = time.perf_counter()
+    text = ft.fetch()
+    ph['text_d2h'] = time.perf_counter() - t
     t = time.perf_counter()
     with open(os.path.join(a.dir, 'out.fa'), 'wb') as fh:
         fh.write(text)
@@ -68,6 +72,13 @@ def main():
     ph['write'] = time.perf_counter() - t
     total = time.perf_counter() - t0
     kernel_ms = ex.time(10)
+    text_ms = ft.time(10)
+    # host render of the fetched payloads (the previous CLI path) must agree
+    nuc, noff, pep, poff = ex.fetch()
+    t = time.perf_counter()
+    host_text = plan.render(nuc, noff, pep, poff)
+    host_render_s = time.perf_counter() - t
+    text_match = host_text == text.tobytes()
     # payload check against the C oracle on the same tables
     from oracle import cds_oracle
     ex_t, tx_t = plan.exons, plan.txs
@@ -94,8 +105,9 @@ def main():
            'records': int(len(plan.txs)), 'intervals': int(len(plan.exons)),
            'cds_bases': int(w.cds_bases), 'output_bytes': len(text) + 1,
            'gff_lines': None, 'phases_s': ph, 'end_to_end_s': total,
-           'kernel_ms_hip_events': kernel_ms, 'generate_files_s': t_gen,
-           'payload_check': ok}
+           'kernel_ms_hip_events': kernel_ms, 'text_assembly_ms_hip_events': text_ms,
+           'host_render_s_reference_point': host_render_s, 'generate_files_s': t_gen,
+           'payload_check': ok, 'device_text_equals_host_render': text_match}
     print(json.dumps(rec), flush=True)
 
 

@@ -395,3 +395,65 @@ def test_orf6_over_extraction_plan_vs_oracle():
     o6.close()
     plan.close()
     dev.close()
+
+
+# ---------------------------------------------------------------------------
+# FASTA text assembly on device (magot_fasta_text_*)
+# ---------------------------------------------------------------------------
+
+def _device_text(fasta, gff, seq_type, order='py2'):
+    gs = G.GenomeSequence(fasta)
+    names = list(gs)
+    dev = engine.DeviceGenome([(n, gs[n]) for n in names])
+    plan = engine.GffPlan.build(G.ensure_file(gff).read(), names, [len(gs[n]) for n in names],
+                                protein=seq_type == 'protein', order=order)
+    assert plan is not None
+    ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
+                               engine.OUT_PEP if seq_type == 'protein' else engine.OUT_NUC)
+    text = engine.FastaText(plan, ex)
+    ex.execute()
+    text.execute()
+    got = text.fetch().tobytes()
+    text.execute()  # idempotent re-run on the same buffers
+    again = text.fetch().tobytes()
+    host = plan.render(*ex.fetch())
+    assert text.time(2) > 0
+    text.close()
+    ex.close()
+    plan.close()
+    assert got == again
+    return got, host
+
+
+@pytest.mark.parametrize('seq_type', ['nucleotide', 'protein'])
+def test_device_text_assembly_vs_oracle(seq_type):
+    """Blank gene records, renamed IDs, X-trimmed peptides, minus strands."""
+    fasta = ('>c1\n' + 'NNNACGTTGCAACGGATCCATGNNNAAA' * 40 + '\n>c2\n' +
+             'GGGAAATTTCCCRYACGT' * 30 + '\n')
+    rows = []
+    for g in range(30):
+        c = 'c1' if g % 3 else 'c2'
+        lo = 1 + 17 * g
+        rows.append('%s\tx\tgene\t%d\t%d\t.\t+\t.\tID=g%d' % (c, lo, lo + 200, g))
+        if g % 4 == 1:
+            continue  # gene without CDS: a blank record
+        s = '+-'[g % 2]
+        rows.append('%s\tx\tmRNA\t%d\t%d\t.\t%s\t.\tID=m%d;Parent=g%d' % (c, lo, lo + 200, s, g, g))
+        for k in range(1 + g % 3):
+            rows.append('%s\tx\tCDS\t%d\t%d\t.\t%s\t0\tID=cds%d;Parent=m%d'
+                        % (c, lo + 40 * k, lo + 40 * k + 30, s, g, g))
+    gff = '\n'.join(rows) + '\n'
+    got, host = _device_text(fasta, gff, seq_type)
+    assert got == host
+    want = mo.gff2fasta(fasta, gff, seq_type=seq_type, order='py2')
+    assert got == want.encode('latin-1')
+    if seq_type == 'protein':
+        assert b'\n>' in got
+
+
+def test_device_text_assembly_obiroi():
+    got, host = _device_text(goldlib.path('O.biroi_refseqGenomeSubset.fasta'),
+                             goldlib.path('O.biroi_NCBIrefseq_gff3Subset.gff'), 'protein')
+    assert got == host
+    want = _json('fixtures.json')['obiroi/protein/py2']
+    assert _sha(got) == want['sha256']
