@@ -1,6 +1,8 @@
 // C ABI of libmagot.so (declarations and contracts: include/magot.h).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -150,6 +152,9 @@ std::vector<uint8_t> genome_meta(const magot_genome* g) {
   return w.buf;
 }
 
+// Pack the contigs on the host and upload the planes (magot_genome_load*).
+int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, magot_genome** out);
+
 }  // namespace
 
 extern "C" {
@@ -218,13 +223,32 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
       set_error("magot_genome_load: null contig pointer");
       return MAGOT_ERR_ARG;
     }
+  std::vector<ContigSource> src(n_contigs);
+  for (uint32_t i = 0; i < n_contigs; ++i) src[i] = ContigSource{seqs[i], lens[i], 0, 0};
+  return load_packed(ctx, src.data(), n_contigs, out);
+}
+
+}  // extern "C"
+
+namespace {
+
+int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, magot_genome** out) {
+  const bool timing = std::getenv("MAGOT_GENOME_TIMING") != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!timing) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "[genome] %-8s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+    t0 = t1;
+  };
   HostPacked hp;
-  pack_genome(seqs, lens, n_contigs, &hp);
+  pack_genome(src, n_contigs, &hp);
+  lap("pack");
   if (hp.runs.size() >= (size_t)kDirClean) {
     set_error("magot_genome_load: too many exception runs");
     return MAGOT_ERR_ARG;
   }
-  if (2 * hp.nib.size() * 4 + 16 > 0xFFFFFFFFull) {  // 32-bit buffer offsets (extract.hip)
+  if (2 * hp.nib_words * 4 + 16 > 0xFFFFFFFFull) {  // 32-bit buffer offsets (extract.hip)
     set_error("magot_genome_load: genomes above 4 Gbases are not supported");
     return MAGOT_ERR_ARG;
   }
@@ -232,7 +256,7 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
   g->ctx = ctx;
   Carve cv;
   // forward + reverse-strand planes, 4 words of slack for window over-reads
-  uint64_t o_nib = cv.take<uint32_t>(2 * hp.nib.size() + 4);
+  uint64_t o_nib = cv.take<uint32_t>(2 * hp.nib_words + 4);
   uint64_t o_runs = cv.take<ExcRun>(hp.runs.size());
   uint64_t o_dir = cv.take<uint32_t>(hp.dir.size());
   MAGOT_HIP_TRY(hipMalloc(&g->arena, cv.used));
@@ -241,8 +265,8 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
   g->nib = reinterpret_cast<uint32_t*>(base + o_nib);
   g->runs = reinterpret_cast<ExcRun*>(base + o_runs);
   g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
-  MAGOT_HIP_TRY(hipMemcpy(g->nib, hp.nib.data(), hp.nib.size() * 4, hipMemcpyHostToDevice));
-  MAGOT_HIP_TRY(hipMemset(g->nib + 2 * hp.nib.size(), 0, 16));
+  MAGOT_HIP_TRY(hipMemcpy(g->nib, hp.nib.get(), hp.nib_words * 4, hipMemcpyHostToDevice));
+  MAGOT_HIP_TRY(hipMemset(g->nib + 2 * hp.nib_words, 0, 16));
   launch_mirror_planes(g->nib, hp.span, ctx->stream);
   MAGOT_HIP_TRY(hipGetLastError());
   MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -257,9 +281,14 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
   g->host_dir = std::move(hp.dir);
   g->extent = hp.extent;
   g->total_bases = hp.extent - kOrigin;
+  lap("upload");
   *out = g.release();
   return MAGOT_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int magot_genome_load_fasta(magot_ctx* ctx, const char* text, uint64_t len, int truncate_names,
                             magot_genome** out) {
@@ -269,21 +298,18 @@ int magot_genome_load_fasta(magot_ctx* ctx, const char* text, uint64_t len, int 
     return MAGOT_ERR_ARG;
   }
   *out = nullptr;
-  std::vector<std::string> names, seqs;
-  if (int rc = parse_fasta(text, len, truncate_names != 0, &names, &seqs)) {
+  FastaContigs fc;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (int rc = scan_fasta(text, len, truncate_names != 0, &fc)) {
     set_error("magot_genome_load_fasta: header needs the Python reader");
     return rc;
   }
-  std::vector<const uint8_t*> ptrs(seqs.size());
-  std::vector<uint64_t> lens(seqs.size());
-  for (size_t i = 0; i < seqs.size(); ++i) {
-    ptrs[i] = reinterpret_cast<const uint8_t*>(seqs[i].data());
-    lens[i] = seqs[i].size();
-  }
+  if (std::getenv("MAGOT_GENOME_TIMING"))
+    fprintf(stderr, "[genome] scan     %.3f s\n",
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   magot_genome* g = nullptr;
-  if (int rc = magot_genome_load(ctx, ptrs.data(), lens.data(), (uint32_t)seqs.size(), &g))
-    return rc;
-  g->names = std::move(names);
+  if (int rc = load_packed(ctx, fc.src.data(), (uint32_t)fc.src.size(), &g)) return rc;
+  g->names = std::move(fc.names);
   *out = g;
   return MAGOT_OK;
 }

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -37,7 +38,9 @@ struct HostPacked {
   // word g >> 3: bits 0-1 code (A C G T = 0..3), bit 2 soft-masked
   // (lower-case), bit 3 exception (byte kept in `runs`, code bits 0).  The
   // device mirrors it into the reverse-strand plane (mirror_planes).
-  std::vector<uint32_t> nib;
+  // Every word is written by the packer (no zero-fill pass).
+  std::unique_ptr<uint32_t[]> nib;
+  uint64_t nib_words = 0;
   uint64_t span = 0;
   std::vector<ExcRun> runs;       // sorted by start, sentinel appended
   std::vector<uint32_t> dir;      // per 4096-block first run with end > block start
@@ -46,13 +49,31 @@ struct HostPacked {
   uint64_t extent = 0;            // first coordinate past the last contig
 };
 
-// FASTA text -> (names, sequences) with GenomeSequence semantics (fasta.cpp);
-// MAGOT_ERR_UNSUPPORTED for headers only the Python reader handles exactly.
-int parse_fasta(const char* text, uint64_t n, bool truncate, std::vector<std::string>* names,
-                std::vector<std::string>* seqs);
+// A contig's bytes: contiguous (width == 0: ptr[0, len)), or still in FASTA
+// line layout -- every line `width` sequence bytes then a `term`-byte line
+// terminator, the last line holding the remainder -- so the packer reads
+// the file text directly.
+struct ContigSource {
+  const uint8_t* ptr;
+  uint64_t len;    // bases
+  uint64_t width;  // 0: contiguous
+  uint32_t term;   // 1 ("\n") or 2 ("\r\n")
+};
 
-// Packs raw contig bytes (multi-threaded host code, pack.cpp).
-void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, HostPacked* out);
+// FASTA text -> contigs with GenomeSequence semantics (fasta.cpp).  Records
+// whose lines are not uniform are stripped into `storage`.  Returns
+// MAGOT_ERR_UNSUPPORTED for headers only the Python reader handles exactly.
+struct FastaContigs {
+  std::vector<std::string> names;
+  std::vector<ContigSource> src;
+  std::vector<std::string> storage;
+};
+int scan_fasta(const char* text, uint64_t n, bool truncate, FastaContigs* out);
+// The contig's bases, contiguous, into dst[0, src.len).
+void copy_contig(const ContigSource& src, uint8_t* dst);
+
+// Packs contig bytes (multi-threaded host code, pack.cpp).
+void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out);
 
 // ---------------------------------------------------------------------------
 // Extraction tiling

@@ -1,17 +1,25 @@
 // Native FASTA reader for the batch path: GenomeSequence.__init__
-// (genome.py:854-877) straight from the file bytes into contig buffers that
-// magot_genome_load packs, without building Python strings.
+// (genome.py:854-877) straight from the file bytes to the packer, without
+// building Python strings or, for the usual fixed-width files, any copy of
+// the sequence at all.
 //
 // Semantics kept: a record starts at every line whose first byte is '>'; its
 // name is the rest of the line without '\r' (truncate_names: the first
-// whitespace-separated word); its sequence is every following line with '\r'
-// and '\n' removed, up to the next '>' line; empty sequences are not stored;
+// whitespace-separated word); its sequence is every following byte except
+// '\r' and '\n', up to the next '>' line; empty sequences are not stored;
 // a repeated name keeps its first position and takes the last non-empty
 // sequence (dict assignment); text before the first '>' is the record "".
 // Headers that Python 3's str.split() would split differently from the
 // reference's Python 2 byte-string split (bytes >= 0x80, 0x1c-0x1f), and
 // empty names under truncate_names (IndexError), return
 // MAGOT_ERR_UNSUPPORTED so the caller uses the Python reader.
+//
+// Layout detection: a record whose CR/LF bytes sit exactly at the ends of
+// equal-width lines (width from its first line) is handed to the packer as
+// a line layout (ContigSource::width); the proof is a count -- the record's
+// non-CR/LF bytes equal what the layout predicts and every predicted
+// terminator byte is CR or LF, so no other byte is.  Other records are
+// stripped into a buffer.  Both passes run on all host threads.
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -23,113 +31,199 @@
 #include "common.h"
 
 namespace magot {
+namespace {
 
-int parse_fasta(const char* text, uint64_t n, bool truncate, std::vector<std::string>* names,
-                std::vector<std::string>* seqs) {
-  struct Rec {
-    std::string name;
-    uint64_t b, e;  // body byte range [b, e) in text (lines, with newlines)
+inline bool is_crlf(uint8_t c) { return c == '\n' || c == '\r'; }
+
+unsigned host_threads() {
+  return std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+template <class F>
+void parallel_for(size_t n, F&& f) {
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
   };
-  std::vector<Rec> recs;
-  uint64_t pos = 0;
+  std::vector<std::thread> pool;
+  const unsigned t = (unsigned)std::min<size_t>(host_threads(), n);
+  for (unsigned k = 1; k < t; ++k) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+}
+
+struct Rec {
+  std::string name;
+  uint64_t b, e;             // body byte range [b, e) in the text
+  uint64_t width = 0;        // candidate line layout (0: none)
+  uint32_t term = 0;
+  uint64_t full_lines = 0;   // lines of width + term bytes
+  uint64_t expect = 0;       // sequence bytes the layout predicts
+  std::atomic<uint64_t> seq{0};       // counted sequence (non-CR/LF) bytes
+  std::atomic<bool> layout_ok{true};  // every predicted terminator byte is CR/LF
+  Rec(std::string n, uint64_t b_, uint64_t e_) : name(std::move(n)), b(b_), e(e_) {}
+};
+
+int header_name(const char* text, uint64_t h, uint64_t eol, bool truncate, std::string* name) {
+  std::string head;
+  head.reserve(eol - h);
+  for (uint64_t i = h + 1; i < eol; ++i)
+    if (text[i] != '\r') head.push_back(text[i]);
+  if (truncate) {
+    for (unsigned char c : head)
+      if (c >= 0x80 || (c >= 0x1c && c <= 0x1f)) return MAGOT_ERR_UNSUPPORTED;
+    auto ws = [](char c) {
+      return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
+    };
+    size_t i = 0;
+    while (i < head.size() && ws(head[i])) ++i;
+    size_t j = i;
+    while (j < head.size() && !ws(head[j])) ++j;
+    if (i == j) return MAGOT_ERR_UNSUPPORTED;  // IndexError
+    head = head.substr(i, j - i);
+  }
+  *name = std::move(head);
+  return MAGOT_OK;
+}
+
+// The line layout a record would have, from its first line and its length.
+void candidate_layout(const char* text, Rec& r) {
+  const uint64_t lb = r.e - r.b;
+  const char* nl = static_cast<const char*>(memchr(text + r.b, '\n', lb));
+  if (!nl) return;  // one unterminated line: contiguous if it holds no '\r'
+  const uint64_t raw = (uint64_t)(nl - text) - r.b;
+  const uint32_t t = raw && text[r.b + raw - 1] == '\r' ? 2 : 1;
+  const uint64_t w = raw + 1 - t;
+  if (!w) return;
+  const uint64_t full = lb / (w + t), rem = lb % (w + t);
+  uint64_t last = rem;  // sequence bytes of a short last line
+  if (rem && is_crlf((uint8_t)text[r.e - 1])) {
+    if (rem <= t) return;  // a blank last line
+    last = rem - t;
+    for (uint32_t j = 0; j < t; ++j)
+      if (!is_crlf((uint8_t)text[r.e - t + j])) return;
+  }
+  r.width = w;
+  r.term = t;
+  r.full_lines = full;
+  r.expect = full * w + last;
+}
+
+}  // namespace
+
+int scan_fasta(const char* text, uint64_t n, bool truncate, FastaContigs* out) {
+  // records: a '>' at a line start opens one
+  std::vector<std::unique_ptr<Rec>> recs;
   std::string name;
   bool have = false;
-  uint64_t body = 0;
-  auto close_rec = [&](uint64_t end) {
-    if (have || end > body) recs.push_back(Rec{name, body, end});
-  };
-  while (pos < n) {
-    if (text[pos] == '>') {
-      close_rec(pos);
-      const char* nl = static_cast<const char*>(memchr(text + pos, '\n', n - pos));
-      const uint64_t eol = nl ? (uint64_t)(nl - text) : n;
-      std::string head;
-      head.reserve(eol - pos);
-      for (uint64_t i = pos + 1; i < eol; ++i)
-        if (text[i] != '\r') head.push_back(text[i]);
-      if (truncate) {
-        for (unsigned char c : head)
-          if (c >= 0x80 || (c >= 0x1c && c <= 0x1f)) return MAGOT_ERR_UNSUPPORTED;
-        size_t i = 0;
-        auto ws = [](char c) {
-          return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
-        };
-        while (i < head.size() && ws(head[i])) ++i;
-        size_t j = i;
-        while (j < head.size() && !ws(head[j])) ++j;
-        if (i == j) return MAGOT_ERR_UNSUPPORTED;  // IndexError
-        head = head.substr(i, j - i);
+  uint64_t body = 0, p = 0;
+  for (;;) {
+    uint64_t h = n;
+    for (uint64_t q = p; q < n;) {
+      const char* f = static_cast<const char*>(memchr(text + q, '>', n - q));
+      if (!f) break;
+      const uint64_t at = (uint64_t)(f - text);
+      if (at == 0 || text[at - 1] == '\n') {
+        h = at;
+        break;
       }
-      name = head;
-      have = true;
-      pos = eol + 1;
-      body = std::min(pos, n);
-      continue;
+      q = at + 1;
     }
-    // skip to the next line that starts with '>'
-    const char* p = text + pos;
-    const char* end = text + n;
-    for (;;) {
-      const char* nl = static_cast<const char*>(memchr(p, '\n', end - p));
-      if (!nl) {
-        pos = n;
-        break;
-      }
-      p = nl + 1;
-      if (p < end && *p == '>') {
-        pos = (uint64_t)(p - text);
-        break;
-      }
-      if (p >= end) {
-        pos = n;
-        break;
-      }
-    }
+    if (have || h > body) recs.emplace_back(new Rec(name, body, h));
+    if (h == n) break;
+    const char* nl = static_cast<const char*>(memchr(text + h, '\n', n - h));
+    const uint64_t eol = nl ? (uint64_t)(nl - text) : n;
+    if (int rc = header_name(text, h, eol, truncate, &name)) return rc;
+    have = true;
+    body = p = std::min(eol + 1, n);
   }
-  close_rec(n);
-  // sequences: line bodies without '\r' / '\n' (records in parallel)
-  std::vector<std::string> body_seq(recs.size());
-  auto work = [&](size_t k) {
-    const Rec& r = recs[k];
-    std::string& s = body_seq[k];
-    s.resize(r.e - r.b);
-    size_t o = 0;
-    for (uint64_t i = r.b; i < r.e; ++i) {
-      const char c = text[i];
-      if (c != '\n' && c != '\r') s[o++] = c;
-    }
-    s.resize(o);
+  for (auto& r : recs) candidate_layout(text, *r);
+
+  // count sequence bytes and check predicted terminators, in chunks
+  constexpr uint64_t kChunk = 8ull << 20;
+  struct Task {
+    Rec* r;
+    uint64_t x, y;
   };
-  {
-    std::vector<std::thread> pool;
-    const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<size_t> order(recs.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
-    std::sort(order.begin(), order.end(),
-              [&](size_t a, size_t b) { return recs[a].e - recs[a].b > recs[b].e - recs[b].b; });
-    std::atomic<size_t> next{0};
-    for (unsigned t = 0; t < hw; ++t)
-      pool.emplace_back([&]() {
-        for (size_t i; (i = next.fetch_add(1)) < order.size();) work(order[i]);
-      });
-    for (auto& t : pool) t.join();
-  }
+  std::vector<Task> tasks;
+  for (auto& r : recs)
+    for (uint64_t x = r->b; x < r->e; x += kChunk)
+      tasks.push_back({r.get(), x, std::min(r->e, x + kChunk)});
+  parallel_for(tasks.size(), [&](size_t i) {
+    const Task& T = tasks[i];
+    Rec& r = *T.r;
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(text);
+    uint64_t crlf = 0;
+    for (uint64_t k = T.x; k < T.y; ++k) crlf += is_crlf(s[k]);
+    r.seq += (T.y - T.x) - crlf;
+    if (!r.width) return;
+    const uint64_t stride = r.width + r.term;
+    // terminators of full lines that start in [x, y)
+    uint64_t line = T.x > r.b ? (T.x - r.b + stride - 1) / stride : 0;
+    bool ok = true;
+    for (uint64_t at = r.b + line * stride; at < T.y && line < r.full_lines;
+         ++line, at += stride)
+      for (uint32_t j = 0; j < r.term; ++j) ok &= is_crlf(s[at + r.width + j]);
+    if (!ok) r.layout_ok = false;
+  });
+
   // dict semantics: first position, last non-empty value
   std::unordered_map<std::string, size_t> at;
-  names->clear();
-  seqs->clear();
-  for (size_t k = 0; k < recs.size(); ++k) {
-    if (body_seq[k].empty()) continue;
-    auto it = at.find(recs[k].name);
+  std::vector<Rec*> chosen;
+  for (auto& r : recs) {
+    if (!r->seq.load()) continue;
+    auto it = at.find(r->name);
     if (it == at.end()) {
-      at.emplace(recs[k].name, names->size());
-      names->push_back(recs[k].name);
-      seqs->push_back(std::move(body_seq[k]));
+      at.emplace(r->name, chosen.size());
+      out->names.push_back(r->name);
+      chosen.push_back(r.get());
     } else {
-      (*seqs)[it->second] = std::move(body_seq[k]);
+      chosen[it->second] = r.get();
     }
   }
+  const uint8_t* s = reinterpret_cast<const uint8_t*>(text);
+  out->src.resize(chosen.size());
+  std::vector<size_t> strip;
+  for (size_t i = 0; i < chosen.size(); ++i) {
+    Rec& r = *chosen[i];
+    const uint64_t len = r.seq.load();
+    if (len == r.e - r.b) {
+      out->src[i] = ContigSource{s + r.b, len, 0, 0};
+    } else if (r.width && r.layout_ok.load() && len == r.expect) {
+      out->src[i] = ContigSource{s + r.b, len, r.width, r.term};
+    } else {
+      out->src[i] = ContigSource{nullptr, len, 0, 0};
+      strip.push_back(i);
+    }
+  }
+  out->storage.assign(strip.size(), std::string());
+  parallel_for(strip.size(), [&](size_t k) {
+    const size_t i = strip[k];
+    const Rec& r = *chosen[i];
+    std::string& dst = out->storage[k];
+    dst.resize(out->src[i].len);
+    size_t o = 0;
+    for (uint64_t j = r.b; j < r.e; ++j)
+      if (!is_crlf(s[j])) dst[o++] = (char)s[j];
+  });
+  for (size_t k = 0; k < strip.size(); ++k)
+    out->src[strip[k]].ptr = reinterpret_cast<const uint8_t*>(out->storage[k].data());
   return MAGOT_OK;
+}
+
+void copy_contig(const ContigSource& src, uint8_t* dst) {
+  if (!src.width) {
+    if (src.len) memcpy(dst, src.ptr, src.len);
+    return;
+  }
+  const uint8_t* p = src.ptr;
+  for (uint64_t left = src.len; left;) {
+    const uint64_t k = std::min(left, src.width);
+    memcpy(dst, p, k);
+    dst += k;
+    p += src.width + src.term;
+    left -= k;
+  }
 }
 
 }  // namespace magot
@@ -141,33 +235,32 @@ extern "C" int magot_fasta_read(const char* text, uint64_t len, int truncate_nam
     magot::set_error("magot_fasta_read: null argument");
     return MAGOT_ERR_ARG;
   }
-  std::vector<std::string> nm, sq;
-  if (int rc = magot::parse_fasta(text, len, truncate_names != 0, &nm, &sq)) {
+  magot::FastaContigs fc;
+  if (int rc = magot::scan_fasta(text, len, truncate_names != 0, &fc)) {
     magot::set_error("magot_fasta_read: header needs the Python reader");
     return rc;
   }
-  *n = (uint32_t)nm.size();
+  const size_t k = fc.names.size();
+  *n = (uint32_t)k;
   uint64_t need_names = 0, need_seqs = 0;
-  for (size_t i = 0; i < nm.size(); ++i) {
-    need_names += nm[i].size() + 1;
-    need_seqs += sq[i].size();
-    if (lens) lens[i] = sq[i].size();
+  std::vector<uint64_t> at(k);
+  for (size_t i = 0; i < k; ++i) {
+    need_names += fc.names[i].size() + 1;
+    at[i] = need_seqs;
+    need_seqs += fc.src[i].len;
+    if (lens) lens[i] = fc.src[i].len;
   }
   if (names_len) *names_len = need_names;
   if ((names && names_cap < need_names) || (seqs && seqs_cap < need_seqs)) {
     magot::set_error("magot_fasta_read: buffer too small");
     return MAGOT_ERR_ARG;
   }
-  for (size_t i = 0; i < nm.size(); ++i) {
-    if (names) {
-      memcpy(names, nm[i].data(), nm[i].size());
-      names += nm[i].size();
+  if (names)
+    for (size_t i = 0; i < k; ++i) {
+      memcpy(names, fc.names[i].data(), fc.names[i].size());
+      names += fc.names[i].size();
       *names++ = '\0';
     }
-    if (seqs) {
-      memcpy(seqs, sq[i].data(), sq[i].size());
-      seqs += sq[i].size();
-    }
-  }
+  if (seqs) magot::parallel_for(k, [&](size_t i) { magot::copy_contig(fc.src[i], seqs + at[i]); });
   return MAGOT_OK;
 }

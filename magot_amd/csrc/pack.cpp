@@ -39,67 +39,114 @@ const ByteClass& byte_class() {
 }
 
 // Pack global coordinates [p0, p1) (p0, p1 multiples of 32, so no plane word
-// is shared with another piece).
-void pack_piece(const uint8_t* const* seqs, const HostPacked& layout, uint64_t p0, uint64_t p1,
+// is shared with another piece): every word of the piece is written once,
+// bases accumulated in a register.
+void pack_piece(const ContigSource* src, const HostPacked& layout, uint64_t p0, uint64_t p1,
                 uint32_t* nib, std::vector<ExcRun>* runs) {
   const ByteClass& bc = byte_class();
   const auto& base = layout.contig_base;
   const auto& len = layout.contig_len;
-  size_t n = base.size();
+  const size_t n = base.size();
   // first contig whose end > p0
   size_t c = std::upper_bound(base.begin(), base.end(), p0) - base.begin();
   c = c == 0 ? 0 : c - 1;
   ExcRun cur{0, 0, 0};
   bool open = false;
+  uint64_t aw = p0 >> 3;  // word being accumulated
+  uint32_t acc = 0;
   for (; c < n; ++c) {
-    uint64_t cb = base[c], ce = base[c] + len[c];
+    const uint64_t cb = base[c], ce = base[c] + len[c];
     if (cb >= p1) break;
-    uint64_t lo = std::max(cb, p0), hi = std::min(ce, p1);
+    uint64_t lo = std::max(cb, p0);
+    const uint64_t hi = std::min(ce, p1);
     if (lo >= hi) continue;
-    const uint8_t* s = seqs[c] + (lo - cb);
-    for (uint64_t g = lo; g < hi; ++g) {
-      uint8_t b = *s++;
-      nib[g >> 3] |= (uint32_t)bc.nib[b] << (4 * (g & 7));
-      if (bc.plain[b]) {
-        if (open) {
-          runs->push_back(cur);
-          open = false;
+    const ContigSource& S = src[c];
+    uint64_t pos = lo - cb;
+    while (lo < hi) {
+      const uint8_t* s;
+      uint64_t seg;
+      if (!S.width) {
+        s = S.ptr + pos;
+        seg = hi - lo;
+      } else {  // FASTA line layout: the rest of the current line
+        const uint64_t line = pos / S.width, off = pos - line * S.width;
+        s = S.ptr + line * (S.width + S.term) + off;
+        seg = std::min(S.width - off, hi - lo);
+      }
+      pos += seg;
+      const uint8_t* e = s + seg;
+      for (;;) {
+        // whole words of plain bases: 8 lookups, one store
+        while ((lo & 7) == 0 && e - s >= 8) {
+          uint32_t w = 0;
+          for (int k = 0; k < 8; ++k) w |= (uint32_t)bc.nib[s[k]] << (4 * k);
+          if (w & 0x88888888u) break;  // an exception byte: per-base path
+          if (open) {
+            runs->push_back(cur);
+            open = false;
+          }
+          if ((lo >> 3) != aw) nib[aw] = acc;
+          aw = lo >> 3;
+          acc = w;
+          s += 8;
+          lo += 8;
         }
-      } else {
-        if (open && cur.byte == b && cur.start + cur.len == g && cur.len < 0x7fffffffu) {
-          ++cur.len;
+        if (s == e) break;
+        const uint8_t b = *s;
+        if ((lo >> 3) != aw) {
+          nib[aw] = acc;
+          acc = 0;
+          aw = lo >> 3;
+        }
+        acc |= (uint32_t)bc.nib[b] << (4 * (lo & 7));
+        if (bc.plain[b]) {
+          if (open) {
+            runs->push_back(cur);
+            open = false;
+          }
         } else {
-          if (open) runs->push_back(cur);
-          cur = ExcRun{g, 1, b};
-          open = true;
+          if (open && cur.byte == b && cur.start + cur.len == lo && cur.len < 0x7fffffffu) {
+            ++cur.len;
+          } else {
+            if (open) runs->push_back(cur);
+            cur = ExcRun{lo, 1, b};
+            open = true;
+          }
         }
+        ++s;
+        ++lo;
       }
     }
   }
   if (open) runs->push_back(cur);
+  // the last accumulated word, then the zero words up to p1 (padding)
+  nib[aw] = acc;
+  for (uint64_t w = aw + 1; w < (p1 >> 3); ++w) nib[w] = 0;
 }
 
 }  // namespace
 
-void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, HostPacked* out) {
+void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out) {
   out->contig_base.resize(n);
   out->contig_len.resize(n);
   uint64_t cur = kOrigin;
   for (uint32_t i = 0; i < n; ++i) {
     out->contig_base[i] = cur;
-    out->contig_len[i] = lens[i];
-    cur += lens[i];
+    out->contig_len[i] = src[i].len;
+    cur += src[i].len;
   }
   out->extent = cur;
   const uint64_t padded = cur + 64;
   out->span = (padded + 64 + 31) & ~31ull;
-  out->nib.assign(out->span / 8, 0u);
+  out->nib_words = out->span / 8;
+  out->nib.reset(new uint32_t[out->nib_words]);  // written in full by the pieces
 
-  // Split [0, extent) into 32-aligned pieces for the worker threads.
+  // Split [0, span) into 32-aligned pieces for the worker threads.
   unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));
   const uint64_t min_piece = 1ull << 22;
-  uint64_t npieces = std::max<uint64_t>(1, std::min<uint64_t>(hw * 4, cur / min_piece + 1));
-  uint64_t step = ((cur + npieces - 1) / npieces + 31) & ~31ull;
+  const uint64_t span = out->span;
+  uint64_t npieces = std::max<uint64_t>(1, std::min<uint64_t>(hw * 4, span / min_piece + 1));
+  uint64_t step = ((span + npieces - 1) / npieces + 31) & ~31ull;
   std::vector<std::vector<ExcRun>> piece_runs(npieces);
   std::vector<std::thread> pool;
   std::atomic<uint64_t> next{0};
@@ -107,13 +154,13 @@ void pack_genome(const uint8_t* const* seqs, const uint64_t* lens, uint32_t n, H
     for (;;) {
       uint64_t k = next.fetch_add(1);
       if (k >= npieces) return;
-      uint64_t p0 = k * step, p1 = std::min(cur, p0 + step);
-      if (p0 < p1)
-        pack_piece(seqs, *out, p0, p1, out->nib.data(), &piece_runs[k]);
+      uint64_t p0 = k * step, p1 = std::min(span, p0 + step);
+      if (p0 < p1) pack_piece(src, *out, p0, p1, out->nib.get(), &piece_runs[k]);
     }
   };
   unsigned nthreads = (unsigned)std::min<uint64_t>(hw, npieces);
-  for (unsigned t = 0; t < nthreads; ++t) pool.emplace_back(worker);
+  for (unsigned t = 1; t < nthreads; ++t) pool.emplace_back(worker);
+  worker();
   for (auto& t : pool) t.join();
 
   // Concatenate, merging runs split at piece boundaries.

@@ -4,6 +4,6 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/e2e; mkdir -p $OUT
-timeout -k 10 900 python scripts/e2e_cli.py --config C3 --seq-type protein > $OUT/e2e_protein.json 2> $OUT/e2e.err || { tail -20 $OUT/e2e.err; exit 1; }
-cat $OUT/e2e_protein.json
+MAGOT_GENOME_TIMING=1 MAGOT_GFF_TIMING=1 timeout -k 10 900 python scripts/e2e_cli.py --config C3 --seq-type protein > $OUT/e2e_protein.json 2> $OUT/e2e.err || { tail -20 $OUT/e2e.err; exit 1; }
+cat $OUT/e2e_protein.json; cat $OUT/e2e.err
 rm -rf /tmp/magot_e2e

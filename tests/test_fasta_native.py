@@ -65,3 +65,47 @@ def test_fasta_read_random():
                 continue
             assert want is not None
             assert [(k, v.decode('latin-1')) for k, v in got] == want, repr(text)
+
+
+LAYOUT_CASES = [
+    '>a\n' + 'ACGTACGTAC\n' * 5 + 'ACG\n',          # uniform lines, short last line
+    '>a\r\n' + 'ACGTACGTAC\r\n' * 5 + 'ACG\r\n',    # CRLF
+    '>a\n' + 'ACGTacgtNN\n' * 4,                    # exact multiple of the width
+    '>a\nACGT\nAC',                                 # no final newline
+    '>a\nACGT\nACGT\n\n>b\nAC\n',                   # blank last line
+    '>a\nACGT\n\nACGT\n',                           # blank middle line
+    '>a\nACG\nACGTT\nA\n',                          # a longer later line
+    '>a\nAC\rG\nACGT\n',                            # CR inside a line
+    '>a\nACGT\n\r\nACGT\n',                         # a line holding only CR
+    '>a\nACGT\rACGT\r',                             # CR-only line ends
+    '>a\r\nACGT\r\nACGT\nAC\r\n',                   # mixed terminators
+    '>a\nACGT\nACG\nACGT\n',                        # a short middle line
+    '>a\nACGT\nACGTA',                              # long unterminated last line
+    '>a\nA\nC\nG\n>a\nTT\nT\n',                     # width 1, repeated name
+]
+
+
+@pytest.mark.parametrize('text', LAYOUT_CASES)
+def test_fasta_read_line_layouts(text):
+    """Fixed-width records are packed from the text in place (line layout);
+    anything else is stripped -- both must give GenomeSequence's bytes."""
+    want = dict(G.GenomeSequence(text))
+    got = engine.fasta_read(text)
+    assert [(k, v.decode('latin-1')) for k, v in got] == list(want.items())
+
+
+def test_fasta_read_layout_across_chunks():
+    """A record larger than the scanner's 8 MiB chunks, with one bad line
+    terminator far from the start (forces the strip path) and without."""
+    rng = np.random.default_rng(11)
+    seq = rng.choice(np.frombuffer(b'ACGTacgtN', np.uint8), size=20_000_003)
+    w = 61
+    lines = [seq[i:i + w].tobytes() for i in range(0, len(seq), w)]
+    body = b'\n'.join(lines) + b'\n'
+    cut = body.index(b'\n', 15_000_000)
+    for text in (b'>big\n' + body + b'>s\nAC\n',
+                 b'>big\n' + body[:cut] + b'\r' + body[cut:] + b'>s\nAC\n',   # CRLF once
+                 b'>big\n' + body[:cut] + b'\nT' + body[cut:] + b'>s\nAC\n'):  # width broken
+        got = engine.fasta_read(text)
+        assert got[0][0] == 'big'
+        assert got[0][1] == text.split(b'\n', 1)[1].split(b'\n>s')[0].replace(b'\n', b'').replace(b'\r', b'')
