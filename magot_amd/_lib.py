@@ -86,7 +86,7 @@ def _declare(lib):
         'magot_translate_sizes': (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp]),
         'magot_translate_batch': (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
                                                  _vp, _vp]),
-        'magot_gff_plan': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64,
+        'magot_gff_plan': (ctypes.c_int, [_vp, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.c_char_p), _u64p, ctypes.c_uint32,
                                           ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(_vp),
                                           _u64p, _u64p]),
@@ -113,11 +113,11 @@ def _declare(lib):
         'magot_fasta_text_time': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                                  ctypes.POINTER(ctypes.c_double)]),
         'magot_fasta_text_destroy': (None, [_vp]),
-        'magot_genome_load_fasta': (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_uint64,
+        'magot_genome_load_fasta': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64,
                                                    ctypes.c_int, ctypes.POINTER(_vp)]),
         'magot_genome_contigs': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32), _vp, _vp,
                                                 ctypes.c_uint64, _u64p]),
-        'magot_fasta_read': (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
+        'magot_fasta_read': (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_uint32), _vp, _vp,
                                             ctypes.c_uint64, _u64p, _vp, ctypes.c_uint64]),
     }

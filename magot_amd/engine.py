@@ -16,6 +16,20 @@ def _as_bytes(s):
     return s.encode('latin-1')
 
 
+def _text_view(s):
+    """A uint8 view of text for the native parsers without copying: bytes,
+    bytearray, mmap (genome.read_buffer) or numpy; str is encoded."""
+    if isinstance(s, str):
+        s = s.encode('latin-1')
+    if isinstance(s, np.ndarray):
+        return np.ascontiguousarray(s).view(np.uint8).reshape(-1)
+    return np.frombuffer(s, dtype=np.uint8)
+
+
+def _text_ptr(view):
+    return view.ctypes.data if len(view) else None
+
+
 class DeviceGenome(object):
     """A GenomeSequence packed into HBM (magot_genome_load).
 
@@ -108,10 +122,11 @@ def fasta_read(text, truncate_names=False):
     """Native GenomeSequence reader (magot_fasta_read): [(name, bytes)], or None
     when a header needs the Python reader.  Host only."""
     L = _lib.lib()
-    data = _as_bytes(text)
+    data = _text_view(text)
+    tp = _text_ptr(data)
     n = ctypes.c_uint32()
     nl = ctypes.c_uint64()
-    rc = L.magot_fasta_read(data, len(data), int(bool(truncate_names)), ctypes.byref(n), None,
+    rc = L.magot_fasta_read(tp, len(data), int(bool(truncate_names)), ctypes.byref(n), None,
                             None, 0, ctypes.byref(nl), None, 0)
     if rc == _lib.ERR_UNSUPPORTED:
         return None
@@ -119,11 +134,11 @@ def fasta_read(text, truncate_names=False):
     lens = np.zeros(max(n.value, 1), dtype=np.uint64)
     names = np.zeros(max(nl.value, 1), dtype=np.uint8)
     seqs = np.zeros(max(int(lens.sum()), 1), dtype=np.uint8)
-    check(L.magot_fasta_read(data, len(data), int(bool(truncate_names)), ctypes.byref(n),
+    check(L.magot_fasta_read(tp, len(data), int(bool(truncate_names)), ctypes.byref(n),
                              ptr(lens), ptr(names), nl.value, ctypes.byref(nl), None, 0),
           'magot_fasta_read')
     seqs = np.zeros(max(int(lens[:n.value].sum()), 1), dtype=np.uint8)
-    check(L.magot_fasta_read(data, len(data), int(bool(truncate_names)), ctypes.byref(n),
+    check(L.magot_fasta_read(tp, len(data), int(bool(truncate_names)), ctypes.byref(n),
                              ptr(lens), ptr(names), nl.value, ctypes.byref(nl), ptr(seqs),
                              len(seqs)), 'magot_fasta_read')
     nms = names[:nl.value].tobytes().split(b'\0')[:n.value]
@@ -145,10 +160,10 @@ class FastaGenome(DeviceGenome):
         self = cls.__new__(cls)
         self.ctx = ctx or _lib.default_context()
         self._keepalive = None
-        data = _as_bytes(text)
+        data = _text_view(text)
         h = ctypes.c_void_p()
-        rc = L.magot_genome_load_fasta(self.ctx.handle, data, len(data), int(bool(truncate_names)),
-                                       ctypes.byref(h))
+        rc = L.magot_genome_load_fasta(self.ctx.handle, _text_ptr(data), len(data),
+                                       int(bool(truncate_names)), ctypes.byref(h))
         if rc == _lib.ERR_UNSUPPORTED:
             return None
         check(rc, 'magot_genome_load_fasta')
@@ -263,7 +278,7 @@ class GffPlan(object):
     @classmethod
     def build(cls, gff, names, lengths, feature='gene', protein=False, order='insertion'):
         L = _lib.lib()
-        text = _as_bytes(gff)
+        text = _text_view(gff)
         n = len(names)
         arr = (ctypes.c_char_p * max(n, 1))(*[_as_bytes(x) for x in names])
         lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
@@ -271,7 +286,7 @@ class GffPlan(object):
             (_lib.GFF_ORDER_PY2 if order == 'py2' else 0)
         h = ctypes.c_void_p()
         ne, nt = ctypes.c_uint64(), ctypes.c_uint64()
-        rc = L.magot_gff_plan(text, len(text), arr, lens.ctypes.data_as(_lib._u64p), n,
+        rc = L.magot_gff_plan(_text_ptr(text), len(text), arr, lens.ctypes.data_as(_lib._u64p), n,
                               _as_bytes(feature), flags, ctypes.byref(h), ctypes.byref(ne),
                               ctypes.byref(nt))
         if rc == _lib.ERR_UNSUPPORTED:

@@ -23,6 +23,7 @@ reproduces the CPython 2.7 dict order the reference's own goldens use
 (``py2order``).
 """
 
+import os
 import sys
 
 import numpy as np
@@ -104,6 +105,18 @@ def read_bytes(potential_file):
         except (OSError, ValueError):
             data = potential_file
     return data if isinstance(data, (bytes, bytearray)) else data.encode('latin-1')
+
+
+def read_buffer(potential_file):
+    """Like read_bytes, but a file on disk is memory-mapped (read-only, no
+    copy): the native parsers read the page cache directly."""
+    if isinstance(potential_file, str) and os.path.isfile(potential_file):
+        import mmap
+        with open(potential_file, 'rb') as fh:
+            if os.fstat(fh.fileno()).st_size == 0:
+                return b''
+            return mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+    return read_bytes(potential_file)
 
 
 def ensure_file(potential_file):

@@ -86,13 +86,13 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order):
     if order not in ('py2', 'insertion'):
         raise ValueError("order must be 'insertion' or 'py2'")
     # the FASTA is read and packed natively; Python reader for unusual headers
-    dev = engine.FastaGenome.load(genome.read_bytes(genome_sequence))
+    dev = engine.FastaGenome.load(genome.read_buffer(genome_sequence))
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)
         dev = seqs.device()
     names = dev.names
     protein = seq_type == 'protein'
-    plan = engine.GffPlan.build(genome.read_bytes(gff), names, [int(x) for x in dev.lengths],
+    plan = engine.GffPlan.build(genome.read_buffer(gff), names, [int(x) for x in dev.lengths],
                                 protein=protein, order=order)
     if plan is None:
         return None

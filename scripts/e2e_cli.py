@@ -38,12 +38,12 @@ def main():
     t_gen = time.perf_counter() - t
     ph = {}
     t0 = time.perf_counter()
-    dev = engine.FastaGenome.load(genome.read_bytes(fa))
+    dev = engine.FastaGenome.load(genome.read_buffer(fa))
     ph['fasta_read_pack_h2d_native'] = time.perf_counter() - t0
     t = time.perf_counter()
     names = dev.names
     protein = a.seq_type == 'protein'
-    plan = engine.GffPlan.build(genome.read_bytes(gf), names, [int(x) for x in dev.lengths],
+    plan = engine.GffPlan.build(genome.read_buffer(gf), names, [int(x) for x in dev.lengths],
                                 protein=protein, order=a.order)
     ph['gff_read_and_plan_native'] = time.perf_counter() - t
     assert plan is not None
