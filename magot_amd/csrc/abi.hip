@@ -924,20 +924,21 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
   uint8_t lut[64];
   if (lut64) std::memcpy(lut, lut64, 64);
   else standard_lut(lut);
-  uint32_t lut16[16];
-  std::memcpy(lut16, lut, 64);
+  uint8_t tables[256];
+  orf6_tables(lut, tables);
   Carve cv;
   const uint64_t o_in = cv.take<uint8_t>(total + 64);
   const uint64_t o_out = cv.take<uint8_t>(total_res + 64);
   const uint64_t o_off = cv.take<uint64_t>(n + 1);
   const uint64_t o_soff = cv.take<uint64_t>(6 * n + 1);
-  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(total_res));
-  const uint64_t o_lut = cv.take<uint8_t>(64);
+  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(total));
+  const uint64_t o_lut = cv.take<uint8_t>(256);
   void* d = nullptr;
   MAGOT_HIP_TRY(hipMalloc(&d, cv.used));
   char* base = static_cast<char*>(d);
   hipError_t e = hipMemcpyAsync(base + o_in, seqs, total, hipMemcpyHostToDevice, ctx->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(base + o_lut, lut, 64, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(base + o_lut, tables, 256, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(base + o_off, seq_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
@@ -945,10 +946,10 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
                        ctx->stream);
   if (e == hipSuccess) {
     uint32_t* wj = reinterpret_cast<uint32_t*>(base + o_wj);
-    launch_orf6_index(reinterpret_cast<const uint64_t*>(base + o_soff), n, wj, ctx->stream);
+    launch_orf6_index(reinterpret_cast<const uint64_t*>(base + o_off), n, wj, ctx->stream);
     launch_orf6(reinterpret_cast<const uint8_t*>(base + o_in),
-                reinterpret_cast<const uint64_t*>(base + o_off), n,
-                reinterpret_cast<const uint64_t*>(base + o_soff), total_res, wj,
+                reinterpret_cast<const uint64_t*>(base + o_off), n, total,
+                reinterpret_cast<const uint64_t*>(base + o_soff), wj,
                 reinterpret_cast<const uint8_t*>(base + o_lut),
                 reinterpret_cast<uint8_t*>(base + o_out), ctx->stream);
     e = hipGetLastError();
@@ -970,12 +971,14 @@ struct magot_orf6 {
   void* arena = nullptr;
   const uint64_t* noff = nullptr;
   const uint64_t* soff = nullptr;
-  uint32_t* wave_j0 = nullptr;
-  uint8_t* lut_dev = nullptr;
+  uint32_t* tile_r0 = nullptr;
+  uint8_t* tables = nullptr;
   uint8_t* out = nullptr;
-  uint64_t n_rec = 0, total = 0;
+  uint64_t n_rec = 0, total = 0, total_nuc = 0;
   std::vector<uint64_t> host_soff;
-  uint32_t lut16[16];
+  void launch(hipStream_t s) const {
+    launch_orf6(plan->args.nuc, noff, n_rec, total_nuc, soff, tile_r0, tables, out, s);
+  }
 };
 
 int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_orf6** out,
@@ -994,16 +997,17 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   if (int rc = magot_orf6_sizes(p->nuc_off.data(), o->n_rec, o->host_soff.data(), nullptr, nullptr))
     return rc;
   o->total = o->host_soff.back();
-  uint8_t lut[64];
+  o->total_nuc = p->nuc_off.back();
+  uint8_t lut[64], tables[256];
   if (lut64) std::memcpy(lut, lut64, 64);
   else standard_lut(lut);
-  std::memcpy(o->lut16, lut, 64);
+  orf6_tables(lut, tables);
   Carve cv;
   const uint64_t o_off = cv.take<uint64_t>(o->n_rec + 1);
   const uint64_t o_soff = cv.take<uint64_t>(6 * o->n_rec + 1);
   const uint64_t o_out = cv.take<uint8_t>(o->total + 64);
-  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(o->total));
-  const uint64_t o_lut = cv.take<uint8_t>(64);
+  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(o->total_nuc));
+  const uint64_t o_lut = cv.take<uint8_t>(256);
   MAGOT_HIP_TRY(hipMalloc(&o->arena, cv.used));
   char* base = static_cast<char*>(o->arena);
   o->noff = reinterpret_cast<const uint64_t*>(base + o_off);
@@ -1013,10 +1017,10 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
                           hipMemcpyHostToDevice));
   MAGOT_HIP_TRY(hipMemcpy(base + o_soff, o->host_soff.data(), (6 * o->n_rec + 1) * 8,
                           hipMemcpyHostToDevice));
-  o->wave_j0 = reinterpret_cast<uint32_t*>(base + o_wj);
-  o->lut_dev = reinterpret_cast<uint8_t*>(base + o_lut);
-  MAGOT_HIP_TRY(hipMemcpy(o->lut_dev, lut, 64, hipMemcpyHostToDevice));
-  launch_orf6_index(o->soff, o->n_rec, o->wave_j0, ctx->stream);
+  o->tile_r0 = reinterpret_cast<uint32_t*>(base + o_wj);
+  o->tables = reinterpret_cast<uint8_t*>(base + o_lut);
+  MAGOT_HIP_TRY(hipMemcpy(o->tables, tables, 256, hipMemcpyHostToDevice));
+  launch_orf6_index(o->noff, o->n_rec, o->tile_r0, ctx->stream);
   MAGOT_HIP_TRY(hipGetLastError());
   MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   if (total_res) *total_res = o->total;
@@ -1030,8 +1034,7 @@ int magot_orf6_execute(magot_ctx* ctx, magot_orf6* o) {
     set_error("magot_orf6_execute: null handle");
     return MAGOT_ERR_ARG;
   }
-  launch_orf6(o->plan->args.nuc, o->noff, o->n_rec, o->soff, o->total, o->wave_j0, o->lut_dev,
-              o->out, ctx->stream);
+  o->launch(ctx->stream);
   MAGOT_HIP_TRY(hipGetLastError());
   return MAGOT_OK;
 }
@@ -1063,8 +1066,7 @@ int magot_orf6_time(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms) {
   double total = 0;
   for (int i = 0; i < iters; ++i) {
     MAGOT_HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-    launch_orf6(o->plan->args.nuc, o->noff, o->n_rec, o->soff, o->total, o->wave_j0, o->lut_dev,
-                o->out, ctx->stream);
+    o->launch(ctx->stream);
     MAGOT_HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     MAGOT_HIP_TRY(hipEventSynchronize(ctx->ev1));
     float ms = 0;

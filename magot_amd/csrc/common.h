@@ -136,14 +136,17 @@ void launch_mirror_planes(uint32_t* nib, uint64_t span, hipStream_t s);
 void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t total,
                     uint8_t* out, hipStream_t s);
 // Six translations per record for Sequence.get_orfs (orf6_kernel): stream
-// j = 6*record + 2*frame + (strand == '+'), soff = 6*n_rec+1 residue offsets.
-// wave_j0 (orf6_index_words(total) u32): the stream of every wave's first
-// residue, filled once per stream table by launch_orf6_index.
-uint64_t orf6_index_words(uint64_t total);
-void launch_orf6_index(const uint64_t* soff, uint64_t n_rec, uint32_t* wave_j0, hipStream_t s);
-void launch_orf6(const uint8_t* nuc, const uint64_t* noff, uint64_t n_rec, const uint64_t* soff,
-                 uint64_t total, const uint32_t* wave_j0, const uint8_t* lut64_dev, uint8_t* out,
-                 hipStream_t s);
+// j = 6*record + 2*frame + (strand == '+'), soff = 6*n_rec+1 padded residue
+// offsets; noff = n_rec+1 offsets of the records in nuc (total_nuc bytes,
+// readable up to the next 16-byte boundary).  tile_r0 (orf6_index_words(
+// total_nuc) u32): the record at every tile start, filled once per record
+// table by launch_orf6_index.  tables_dev: 256 bytes from orf6_tables.
+uint64_t orf6_index_words(uint64_t total_nuc);
+void orf6_tables(const uint8_t lut64[64], uint8_t out[256]);
+void launch_orf6_index(const uint64_t* noff, uint64_t n_rec, uint32_t* tile_r0, hipStream_t s);
+void launch_orf6(const uint8_t* nuc, const uint64_t* noff, uint64_t n_rec, uint64_t total_nuc,
+                 const uint64_t* soff, const uint32_t* tile_r0, const uint8_t* tables_dev,
+                 uint8_t* out, hipStream_t s);
 void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const int32_t* frames,
                       const uint8_t* strands, const uint64_t* pep_off, uint64_t total_pep,
                       const uint32_t* lut16, uint8_t* out, hipStream_t s);

@@ -368,6 +368,23 @@ def test_orf6_batch_vs_oracle():
         assert six == _oracle_six(s), s[:40]
 
 
+def test_orf6_batch_tile_shapes_vs_oracle():
+    """Tile edge cases of the input-stationary kernel: hundreds of tiny
+    records in one tile (several record batches), records longer than a tile
+    (chunks owned by different tiles, both strands), and a record ending
+    exactly at the end of the batch."""
+    rng = np.random.default_rng(47)
+    alphabet = np.frombuffer(b'ACGTACGTACGTacgtNnRY', dtype=np.uint8)
+    lens = [int(x) for x in rng.integers(0, 12, size=900)]
+    lens += [3968, 3967, 3969, 7936, 12_345, 20_001] + [int(x) for x in rng.integers(0, 9000, 40)]
+    lens += [int(x) for x in rng.integers(0, 7, size=500)]
+    seqs = [alphabet[rng.integers(0, len(alphabet), size=L)].tobytes().decode('latin-1')
+            for L in lens]
+    got = engine.orf6_batch(seqs)
+    for i, (s, six) in enumerate(zip(seqs, got)):
+        assert six == _oracle_six(s), (i, len(s))
+
+
 def test_orf6_over_extraction_plan_vs_oracle():
     """C5 shape at small size: gather + six-frame translation, all in HBM."""
     w = synth.make('small', seed=43, genome_bases=1_000_000, n_tx=400, iupac_rate=2e-3)
