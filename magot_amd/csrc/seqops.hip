@@ -165,8 +165,9 @@ __global__ __launch_bounds__(kOpsThreads) void translate_kernel(
 // ---------------------------------------------------------------------------
 constexpr int64_t kOrfTile = 3968;  // bases per wave tile: + halo and alignment = 256 x 16 B
 constexpr int kOrfVecs = 256;       // staged 16-byte vectors per wave
-constexpr int kOrfBatch = 32;       // records per segment batch
+constexpr int kOrfBatch = 16;       // records per segment batch
 constexpr int kOrfSegs = 6 * kOrfBatch;
+constexpr int kOrfRankWords = 128;  // chunk bitmap: a batch owns < 4096 chunks
 
 // real codons of frame f in a record of L bases (0 when translate() is None)
 __device__ __host__ __forceinline__ uint64_t orf_count(uint64_t L, uint32_t f) {
@@ -184,22 +185,36 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_index_kernel(const uint64_t*
     tile_r0[t] = (uint32_t)r;
 }
 
+// A run of output chunks of one stream, rebased so that the wave-wide chunk
+// number q addresses it directly: chunk q writes out0 + 16q from staged
+// position p0 + 48q ('+', residues ascending) or p0 - 48q ('-', first
+// residue at the highest codon), |rem0| - 16q residues left.
 struct OrfSeg {
-  uint64_t out0;  // output byte of the segment's first chunk
-  int32_t p0;     // staged position of its first residue's codon
-  int32_t rem0;   // residues from there to the stream's end; < 0: '-' strand
+  uint64_t out0;
+  int32_t p0;
+  int32_t rem0;  // < 0: '-' strand
 };
+
+__device__ __forceinline__ uint64_t div48(uint64_t v) {
+  return v < (1ull << 32) ? (uint64_t)((uint32_t)v / 48u) : v / 48;
+}
 
 __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
     const uint8_t* __restrict__ nuc, const uint64_t* __restrict__ noff, uint64_t n_rec,
     uint64_t total, const uint64_t* __restrict__ soff, const uint32_t* __restrict__ tile_r0,
     const uint8_t* __restrict__ tables, uint64_t n_tiles, uint8_t* __restrict__ out) {
-  __shared__ uint32_t s_tbl[64];  // bytes: [0,128) '+', [128,256) '-'
+  __shared__ uint8_t s_tbl[256];   // residue of cidx: [0,128) '+', [128,256) '-'
+  __shared__ uint8_t s_code[256];  // byte -> 2-bit code, or 0x40 when not ACGTacgt
   __shared__ uint4 s_stage[kOpsThreads / 64][kOrfVecs];
   __shared__ OrfSeg s_seg[kOpsThreads / 64][kOrfSegs];
-  __shared__ uint32_t s_start[kOpsThreads / 64][kOrfSegs + 1];
+  __shared__ uint32_t s_bm[kOpsThreads / 64][kOrfRankWords];
+  __shared__ uint32_t s_pre[kOpsThreads / 64][kOrfRankWords];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x < 64) s_tbl[threadIdx.x] = reinterpret_cast<const uint32_t*>(tables)[threadIdx.x];
+  s_tbl[threadIdx.x] = tables[threadIdx.x];
+  {
+    const uint32_t c = code_of(threadIdx.x);
+    s_code[threadIdx.x] = (uint8_t)(c < 4 ? c : 0x40u);
+  }
   __syncthreads();
   const uint64_t tile = (uint64_t)blockIdx.x * (kOpsThreads / 64) + wave;
   if (tile >= n_tiles) return;  // wave-uniform
@@ -207,23 +222,26 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
   const uint64_t W0 = (T0 >= 48 ? T0 - 48 : 0) & ~15ull;
   const uint64_t WE = min(T1 + 50, total);
   const uint32_t nvec = (uint32_t)((WE - W0 + 15) / 16);
-  // staging loads first (one memory latency), converted after the record reads
+  // raw staging: all loads in flight at once, stored to LDS when they land;
+  // converted to codon indices in place after the record reads
   constexpr int kPer = kOrfVecs / 64;
-  uint4 v[kPer];
-  uint32_t nx[kPer];
+  {
+    uint4 v[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const uint32_t t = min((uint32_t)(lane + 64 * k), nvec - 1);
-    v[k] = *reinterpret_cast<const uint4*>(nuc + W0 + 16 * (uint64_t)t);
-    nx[k] = *reinterpret_cast<const uint32_t*>(nuc + W0 + 16 * (uint64_t)min(t + 1, nvec - 1));
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t t = min((uint32_t)(lane + 64 * k), nvec - 1);
+      v[k] = *reinterpret_cast<const uint4*>(nuc + W0 + 16 * (uint64_t)t);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) s_stage[wave][lane + 64 * k] = v[k];
   }
   const uint8_t* const stage = reinterpret_cast<const uint8_t*>(s_stage[wave]);
-  const uint8_t* const tbl = reinterpret_cast<const uint8_t*>(s_tbl);
   OrfSeg* const seg = s_seg[wave];
-  uint32_t* const start = s_start[wave];
+  uint32_t* const bm = s_bm[wave];
+  uint32_t* const pre = s_pre[wave];
   bool staged = false;
   for (uint64_t rb = tile_r0[tile];; rb += kOrfBatch) {
-    // ---- this batch's segments: lane < kOrfBatch owns record rb + lane
+    // ---- the batch's segments: lane < kOrfBatch owns record rb + lane
     const uint64_t r = rb + (uint64_t)lane;
     uint64_t nb = 0, L = 0;
     const bool rec = lane < kOrfBatch && r < n_rec;
@@ -232,104 +250,145 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
       L = noff[r + 1] - nb;
     }
     const bool mine = rec && nb < T1;
-    uint32_t cnt[6];
-    uint32_t lane_total = 0;
+    uint32_t cnt[6], lo_c[6], nres_c[6];
+    uint32_t lane_total = 0, lane_segs = 0;
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
       const uint32_t f = (uint32_t)s >> 1;
-      const bool plus = s & 1;
-      const int64_t nres = mine ? (int64_t)orf_count(L, f) : 0;
-      const int64_t nch = (nres + 15) / 16;
-      int64_t lo = 0, hi = 0, p = 0;
-      if (plus) {  // chunk c's first codon starts at x0 + 48c
-        const int64_t x0 = (int64_t)(nb + 2 * f);
-        lo = (int64_t)T0 > x0 ? ((int64_t)T0 - x0 + 47) / 48 : 0;
-        hi = (int64_t)T1 > x0 ? ((int64_t)T1 - x0 + 47) / 48 : 0;
-        p = x0 + 48 * lo;
-      } else {  // chunk c's first codon (read backwards) lies at x0 - 48c
-        const int64_t x0 = (int64_t)(nb + L) - 3 - 2 * (int64_t)f;
-        lo = x0 >= (int64_t)T1 ? (x0 - (int64_t)T1) / 48 + 1 : 0;
-        hi = x0 >= (int64_t)T0 ? (x0 - (int64_t)T0) / 48 + 1 : 0;
-        p = x0 - 48 * lo;
+      const uint64_t nres = mine ? orf_count(L, f) : 0;
+      const uint64_t nch = (nres + 15) / 16;
+      uint64_t lo, hi;
+      if (s & 1) {  // '+': chunk c's first codon starts at x0 + 48c
+        const uint64_t x0 = nb + 2 * f;
+        lo = T0 > x0 ? div48(T0 - x0 + 47) : 0;
+        hi = T1 > x0 ? div48(T1 - x0 + 47) : 0;
+      } else {  // '-': chunk c's first codon (read backwards) lies at x0 - 48c
+        const uint64_t x0 = nb + L - 3 - 2 * f;  // only used when nres > 0
+        lo = x0 >= T1 ? div48(x0 - T1) + 1 : 0;
+        hi = x0 >= T0 ? div48(x0 - T0) + 1 : 0;
       }
-      hi = min(hi, nch);
+      hi = nres ? min(hi, nch) : 0;
       lo = min(lo, hi);
       cnt[s] = (uint32_t)(hi - lo);
-      if (cnt[s]) {
-        const uint64_t j = 6 * r + (uint64_t)s;
-        OrfSeg g;
-        g.out0 = soff[j] + 16 * (uint64_t)lo;
-        g.p0 = (int32_t)((int64_t)p - (int64_t)W0);
-        const int32_t rem = (int32_t)(nres - 16 * lo);
-        g.rem0 = plus ? rem : -rem;
-        seg[6 * lane + s] = g;
-      }
+      lo_c[s] = (uint32_t)lo;
+      nres_c[s] = (uint32_t)nres;
       lane_total += cnt[s];
+      lane_segs += cnt[s] != 0;
     }
-    // wave-inclusive scan of the lane totals
-    uint32_t incl = lane_total;
+    // wave-inclusive scans: chunk starts and compacted segment slots
+    uint32_t incl = lane_total, incl_s = lane_segs;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += y;
-    }
-    const uint32_t n_chunks = __shfl(incl, 63, 64);
-    if (lane < kOrfBatch) {
-      uint32_t acc = incl - lane_total;
-#pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        start[6 * lane + s] = acc;
-        acc += cnt[s];
+      const uint32_t y = __shfl_up(incl, d, 64), z = __shfl_up(incl_s, d, 64);
+      if (lane >= d) {
+        incl += y;
+        incl_s += z;
       }
     }
-    if (lane == 0) start[kOrfSegs] = n_chunks;
+    const uint32_t n_chunks = __shfl(incl, 63, 64);
     // does the next batch still start inside the tile?
     const bool more = __shfl((int)(rec && nb + L < T1), kOrfBatch - 1, 64) &&
                       rb + kOrfBatch < n_rec;
-    if (!staged) {
-#pragma unroll
+    bm[lane] = 0u;
+    bm[lane + 64] = 0u;
+    if (!staged) {  // cidx[p] = c[p] | c[p+1] << 2 | c[p+2] << 4 | invalid << 6
+      // in place, vector t after vector t+1's first bytes were read (LDS
+      // operations of a wave complete in order)
+#pragma unroll 1
       for (int k = 0; k < kPer; ++k) {
         const uint32_t t = lane + 64 * k;
-        const uint32_t w[5] = {v[k].x, v[k].y, v[k].z, v[k].w, nx[k]};
-        uint32_t c[18];
+        const uint4 raw = s_stage[wave][t];
+        const uint32_t nxt = reinterpret_cast<const uint32_t*>(s_stage[wave])[4 * min(t + 1, (uint32_t)kOrfVecs - 1)];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t w[5] = {raw.x, raw.y, raw.z, raw.w, nxt};
+        uint32_t e[5];
 #pragma unroll
-        for (int i = 0; i < 18; ++i) c[i] = code_of((w[i >> 2] >> (8 * (i & 3))) & 0xFFu);
-        uint32_t o[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const uint32_t x = (c[i] & 3u) | ((c[i + 1] & 3u) << 2) | ((c[i + 2] & 3u) << 4) |
-                             (((c[i] | c[i + 1] | c[i + 2]) & 4u) << 4);
-          o[i >> 2] |= x << (8 * (i & 3));
+        for (int j = 0; j < 5; ++j) {
+          const uint32_t x = w[j];
+          e[j] = (uint32_t)s_code[x & 0xFFu] | ((uint32_t)s_code[(x >> 8) & 0xFFu] << 8);
+          if (j < 4)
+            e[j] |= ((uint32_t)s_code[(x >> 16) & 0xFFu] << 16) | ((uint32_t)s_code[x >> 24] << 24);
         }
-        if (t < nvec) s_stage[wave][t] = make_uint4(o[0], o[1], o[2], o[3]);
+        uint32_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t e1 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 1);
+          const uint32_t e2 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 2);
+          o[j] = (e[j] & 0x03030303u) | ((e1 & 0x03030303u) << 2) | ((e2 & 0x03030303u) << 4) |
+                 ((e[j] | e1 | e2) & 0x40404040u);
+        }
+        s_stage[wave][t] = make_uint4(o[0], o[1], o[2], o[3]);
+        __builtin_amdgcn_wave_barrier();
       }
       staged = true;
     }
     __builtin_amdgcn_wave_barrier();
+    if (lane < kOrfBatch) {
+      uint32_t start = incl - lane_total, slot = incl_s - lane_segs;
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {
+        if (!cnt[s]) continue;
+        const uint32_t f = (uint32_t)s >> 1;
+        const bool plus = s & 1;
+        const uint64_t lo = lo_c[s];
+        const int64_t p = plus ? (int64_t)(nb + 2 * f + 48 * lo)
+                               : (int64_t)(nb + L - 3 - 2 * f - 48 * lo);
+        OrfSeg g;
+        g.out0 = soff[6 * r + (uint64_t)s] + 16 * lo - 16 * (uint64_t)start;
+        g.p0 = (int32_t)(p - (int64_t)W0 + (plus ? -48 : 48) * (int64_t)start);
+        const int32_t rem = (int32_t)(nres_c[s] - 16 * lo) + 16 * (int32_t)start;
+        g.rem0 = plus ? rem : -rem;
+        seg[slot++] = g;
+        atomicOr(&bm[start >> 5], 1u << (start & 31));
+        start += cnt[s];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    {  // pre[w] = segment starts in words before w
+      const uint32_t a = __popc(bm[2 * lane]), b = __popc(bm[2 * lane + 1]);
+      uint32_t x = a + b;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      pre[2 * lane] = x - a - b;
+      pre[2 * lane + 1] = x - b;
+    }
+    __builtin_amdgcn_wave_barrier();
     // ---- the batch's chunks, 64 at a time
     for (uint32_t q = lane; q < n_chunks; q += 64) {
-      uint32_t a = 0, b = kOrfSegs;  // last segment with start <= q (and chunks)
-      while (b - a > 1) {
-        const uint32_t m = (a + b) >> 1;
-        if (start[m] <= q) a = m;
-        else b = m;
-      }
-      const OrfSeg g = seg[a];
-      const uint32_t k = q - start[a];
+      const uint32_t wq = q >> 5;
+      const uint32_t rank = pre[wq] + __popc(bm[wq] & (0xFFFFFFFFu >> (31 - (q & 31))));
+      const OrfSeg g = seg[rank - 1];
       const bool minus = g.rem0 < 0;
-      const int32_t rem = (minus ? -g.rem0 : g.rem0) - 16 * (int32_t)k;
-      const int32_t nr = min(16, rem);
-      const int32_t step = minus ? -3 : 3;
-      const int32_t p = g.p0 + 16 * step * (int32_t)k;
-      const uint32_t toff = minus ? 128u : 0u;
+      const int32_t rem = (minus ? -g.rem0 : g.rem0) - 16 * (int32_t)q;
+      const int32_t p = g.p0 + (minus ? -48 : 48) * (int32_t)q;
+      // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed below)
+      const uint8_t* const src = stage + (minus ? p - 45 : p);
+      const uint8_t* const tb = s_tbl + (minus ? 128 : 0);
       uint32_t o[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int32_t pi = min(max(p + step * min(i, nr - 1), 0), 16 * kOrfVecs - 1);
-        const uint32_t aa = tbl[toff + stage[pi]];
-        o[i >> 2] |= aa << (8 * (i & 3));
+      for (int i = 0; i < 16; ++i) o[i >> 2] |= (uint32_t)tb[src[3 * i]] << (8 * (i & 3));
+      if (minus) {
+        const uint32_t t0 = o[0], t1 = o[1];
+        o[0] = __builtin_amdgcn_perm(0u, o[3], 0x00010203u);
+        o[1] = __builtin_amdgcn_perm(0u, o[2], 0x00010203u);
+        o[2] = __builtin_amdgcn_perm(0u, t1, 0x00010203u);
+        o[3] = __builtin_amdgcn_perm(0u, t0, 0x00010203u);
       }
-      *reinterpret_cast<uint4*>(out + g.out0 + 16 * (uint64_t)k) = make_uint4(o[0], o[1], o[2], o[3]);
+      if (rem < 16) {  // stream end: residues past it repeat the last one
+        const uint32_t last = (uint32_t)rem - 1;
+        const uint32_t lw = last >> 2 == 0 ? o[0] : last >> 2 == 1 ? o[1] : last >> 2 == 2 ? o[2] : o[3];
+        const uint32_t fill = ((lw >> (8 * (last & 3))) & 0xFFu) * 0x01010101u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int32_t keep = min(max(rem - 4 * j, 0), 4);  // bytes of word j kept
+          const uint32_t mask = keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
+          o[j] = (o[j] & mask) | (fill & ~mask);
+        }
+      }
+      *reinterpret_cast<uint4*>(out + g.out0 + 16 * (uint64_t)q) = make_uint4(o[0], o[1], o[2], o[3]);
     }
     if (!more) break;
     __builtin_amdgcn_wave_barrier();  // segment tables are rewritten
