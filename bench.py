@@ -256,9 +256,11 @@ def strong_main(args, dist, rank, local, world):
 
 def orf6_main(args, dist, rank, local, world):
     """C5 (BASELINE configs[4]): 3 Gb genome, 2M transcripts; a step gathers
-    every transcript's CDS (extract_kernel, nucleotide output kept in HBM) and
-    produces its six translations (orf6_kernel, Sequence.get_orfs's
-    frame x strand loop).  Weak scaling per rank like the default mode."""
+    every transcript's CDS from the packed genome and produces its six
+    translations (Sequence.get_orfs's frame x strand loop) in ONE kernel
+    (orf6_kernel<genome>: the gather is fused, no nucleotide round trip
+    through HBM).  The extraction plan's own kernel runs only for the
+    nucleotide parity check.  Weak scaling per rank like the default mode."""
     from magot_amd import _lib, engine, synth
     t0 = time.perf_counter()
     w = synth.make(args.config, seed=shard_seed(args.config, rank))
@@ -296,24 +298,22 @@ def orf6_main(args, dist, rank, local, world):
     _, _, slen = o6.fetch()
     R = int(slen.sum())
     for _ in range(args.warmup):
-        plan.execute()
         o6.execute()
     ctx.sync()
     barrier(dist)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        plan.execute()
         o6.execute()
     ctx.sync()
     elapsed = time.perf_counter() - t0
     barrier(dist)
     elapsed_max = allreduce_max(dist, elapsed)
-    k_ex = plan.time(10)
+    k_ex = plan.time(10)  # reported beside: the nucleotide-only extraction
     k_o6 = o6.time(10)
     total_bases = allreduce_sum(dist, float(B))
     # algorithmic bytes: 2-bit genome reads + six translations + descriptors
     alg = -(-B // 4) + R + 16 * int(plan.n_exons) + 32 * int(plan.n_tx)
-    achieved = alg / ((k_ex + k_o6) * 1e-3) / 1e9
+    achieved = alg / (k_o6 * 1e-3) / 1e9
     if rank == 0:
         rec = {
             'metric': 'CDS bases extracted+translated/sec', 'value': total_bases * args.steps /
@@ -327,8 +327,9 @@ def orf6_main(args, dist, rank, local, world):
                        'parallelism': 'contig-sharded x%d (weak)' % world},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
-                         'kernel': 'extract_kernel + orf6_kernel',
-                         'kernel_ms': {'extract': k_ex, 'orf6': k_o6},
+                         'kernel': 'orf6_kernel (gather fused with six-frame translation)',
+                         'kernel_ms': k_o6,
+                         'extract_kernel_ms_nucleotide_only': k_ex,
                          'algorithmic_bytes_per_step': alg},
             'cpu_baseline': None, 'parity': parity, 'phases_s': {'generate': t_gen},
         }

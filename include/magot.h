@@ -221,15 +221,18 @@ int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* s
  * trimX always drops (genome.py:809-821), so it is not emitted; frame 0 is
  * untrimmed (the caller drops one leading 'X').  Streams start on 16-byte
  * boundaries: stream_off (6n+1) are the padded offsets, stream_len (6n) the
- * real residue counts; none_mask[j] = 1 where the reference returns None
- * (len <= 2 + f).  stream_len / none_mask may be NULL.
+ * real residue counts, and the padding bytes are 0; none_mask[j] = 1 where
+ * the reference returns None (len <= 2 + f).  stream_len / none_mask may be
+ * NULL.
  */
 int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,
                      uint64_t* stream_len, uint8_t* none_mask);
 int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
                      const uint8_t* lut64, const uint64_t* stream_off, uint8_t* out);
-/* The same over an extraction plan's nucleotide records, kept in HBM
- * (BASELINE configs[4], C5: gather + six-frame translation). */
+/* The same over an extraction plan's records, in HBM (BASELINE configs[4],
+ * C5): one kernel gathers each record from the packed genome through the
+ * plan's intervals and writes its six translations (the plan's nucleotide
+ * output is not needed). */
 typedef struct magot_orf6 magot_orf6;
 int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_orf6** out,
                     uint64_t* total_res);

@@ -66,6 +66,7 @@ struct magot_plan {
   ExtractArgs args{};
   std::vector<uint64_t> nuc_off, pep_off;  // host copies, n_tx+1
   uint64_t n_exons = 0, n_tx = 0;
+  uint64_t n_ex_c = 0;  // compacted (non-empty) intervals in args.ex_g / ex_out
   bool executed = false;
 };
 
@@ -640,6 +641,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   p->nuc_off = std::move(nuc_off);
   p->pep_off = std::move(pep_off);
   p->n_exons = E;
+  p->n_ex_c = Ec;
   p->n_tx = T;
   if (nuc_bytes) *nuc_bytes = B;
   if (pep_bytes) *pep_bytes = P;
@@ -921,17 +923,20 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
     set_error("magot_orf6_batch: null buffer");
     return MAGOT_ERR_ARG;
   }
-  uint8_t lut[64];
+  uint8_t lut[64], tables[256];
   if (lut64) std::memcpy(lut, lut64, 64);
   else standard_lut(lut);
-  uint8_t tables[256];
   orf6_tables(lut, tables);
+  Orf6Tiles tiles;
+  orf6_plan_tiles(seq_off, n, nullptr, 0, &tiles);
+  const uint64_t n_tiles = tiles.r0.size();
   Carve cv;
   const uint64_t o_in = cv.take<uint8_t>(total + 64);
   const uint64_t o_out = cv.take<uint8_t>(total_res + 64);
   const uint64_t o_off = cv.take<uint64_t>(n + 1);
   const uint64_t o_soff = cv.take<uint64_t>(6 * n + 1);
-  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(total));
+  const uint64_t o_t0 = cv.take<uint64_t>(n_tiles + 1);
+  const uint64_t o_r0 = cv.take<uint32_t>(n_tiles);
   const uint64_t o_lut = cv.take<uint8_t>(256);
   void* d = nullptr;
   MAGOT_HIP_TRY(hipMalloc(&d, cv.used));
@@ -944,14 +949,25 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
   if (e == hipSuccess)
     e = hipMemcpyAsync(base + o_soff, stream_off, (6 * n + 1) * 8, hipMemcpyHostToDevice,
                        ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(base + o_t0, tiles.t0.data(), (n_tiles + 1) * 8, hipMemcpyHostToDevice,
+                       ctx->stream);
+  if (e == hipSuccess && n_tiles)
+    e = hipMemcpyAsync(base + o_r0, tiles.r0.data(), n_tiles * 4, hipMemcpyHostToDevice,
+                       ctx->stream);
   if (e == hipSuccess) {
-    uint32_t* wj = reinterpret_cast<uint32_t*>(base + o_wj);
-    launch_orf6_index(reinterpret_cast<const uint64_t*>(base + o_off), n, wj, ctx->stream);
-    launch_orf6(reinterpret_cast<const uint8_t*>(base + o_in),
-                reinterpret_cast<const uint64_t*>(base + o_off), n, total,
-                reinterpret_cast<const uint64_t*>(base + o_soff), wj,
-                reinterpret_cast<const uint8_t*>(base + o_lut),
-                reinterpret_cast<uint8_t*>(base + o_out), ctx->stream);
+    Orf6Args a{};
+    a.nuc = reinterpret_cast<const uint8_t*>(base + o_in);
+    a.noff = reinterpret_cast<const uint64_t*>(base + o_off);
+    a.n_rec = n;
+    a.total = total;
+    a.soff = reinterpret_cast<const uint64_t*>(base + o_soff);
+    a.tile_t0 = reinterpret_cast<const uint64_t*>(base + o_t0);
+    a.tile_r0 = reinterpret_cast<const uint32_t*>(base + o_r0);
+    a.n_tiles = n_tiles;
+    a.tables = reinterpret_cast<const uint8_t*>(base + o_lut);
+    a.out = reinterpret_cast<uint8_t*>(base + o_out);
+    launch_orf6(a, false, ctx->stream);
     e = hipGetLastError();
   }
   if (e == hipSuccess) e = hipMemcpyAsync(out, base + o_out, total_res, hipMemcpyDeviceToHost, ctx->stream);
@@ -965,27 +981,25 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
   return rc;
 }
 
+// Six frames over an extraction plan: the records are gathered from the
+// genome plane through the plan's intervals inside the kernel (fused; the
+// plan's nucleotide output is not read).
 struct magot_orf6 {
   magot_ctx* ctx = nullptr;
   magot_plan* plan = nullptr;
   void* arena = nullptr;
-  const uint64_t* noff = nullptr;
-  const uint64_t* soff = nullptr;
-  uint32_t* tile_r0 = nullptr;
-  uint8_t* tables = nullptr;
+  Orf6Args args{};
   uint8_t* out = nullptr;
-  uint64_t n_rec = 0, total = 0, total_nuc = 0;
+  uint64_t n_rec = 0, total = 0;
   std::vector<uint64_t> host_soff;
-  void launch(hipStream_t s) const {
-    launch_orf6(plan->args.nuc, noff, n_rec, total_nuc, soff, tile_r0, tables, out, s);
-  }
+  void launch(hipStream_t s) const { launch_orf6(args, true, s); }
 };
 
 int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_orf6** out,
                     uint64_t* total_res) {
   if (int rc = bind(ctx)) return rc;
-  if (!p || !out || !(p->args.outputs & MAGOT_OUT_NUC)) {
-    set_error("magot_plan_orf6: needs a plan with nucleotide output");
+  if (!p || !out) {
+    set_error("magot_plan_orf6: null argument");
     return MAGOT_ERR_ARG;
   }
   *out = nullptr;
@@ -997,7 +1011,29 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   if (int rc = magot_orf6_sizes(p->nuc_off.data(), o->n_rec, o->host_soff.data(), nullptr, nullptr))
     return rc;
   o->total = o->host_soff.back();
-  o->total_nuc = p->nuc_off.back();
+  const uint64_t total_nuc = p->nuc_off.back();
+  // interval rows {unified anchor, start} from the plan's compacted table
+  const uint64_t ne = p->n_ex_c;
+  std::vector<uint64_t> ex_g(ne), ex_out(ne + 1), rows(2 * (ne + 1));
+  if (ne) {
+    MAGOT_HIP_TRY(hipMemcpy(ex_g.data(), p->args.ex_g, ne * 8, hipMemcpyDeviceToHost));
+    MAGOT_HIP_TRY(hipMemcpy(ex_out.data(), p->args.ex_out, (ne + 1) * 8, hipMemcpyDeviceToHost));
+  }
+  const uint64_t span = p->args.span;
+  std::vector<uint64_t> starts(ne + 1);
+  for (uint64_t i = 0; i < ne; ++i) {
+    const uint64_t gw = ex_g[i], o0 = ex_out[i], len = ex_out[i + 1] - o0;
+    const uint64_t gs = gw & ~(kRcBit | kExcBit);
+    rows[2 * i] = (gw & kRcBit) ? 2 * span - gs - len - o0 : gs - o0;
+    rows[2 * i + 1] = o0;
+    starts[i] = o0;
+  }
+  rows[2 * ne] = 0;
+  rows[2 * ne + 1] = total_nuc;
+  starts[ne] = total_nuc;
+  Orf6Tiles tiles;
+  orf6_plan_tiles(p->nuc_off.data(), o->n_rec, starts.data(), ne, &tiles);
+  const uint64_t n_tiles = tiles.r0.size();
   uint8_t lut[64], tables[256];
   if (lut64) std::memcpy(lut, lut64, 64);
   else standard_lut(lut);
@@ -1006,23 +1042,39 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   const uint64_t o_off = cv.take<uint64_t>(o->n_rec + 1);
   const uint64_t o_soff = cv.take<uint64_t>(6 * o->n_rec + 1);
   const uint64_t o_out = cv.take<uint8_t>(o->total + 64);
-  const uint64_t o_wj = cv.take<uint32_t>(orf6_index_words(o->total_nuc));
+  const uint64_t o_rows = cv.take<uint64_t>(2 * (ne + 1));
+  const uint64_t o_t0 = cv.take<uint64_t>(n_tiles + 1);
+  const uint64_t o_r0 = cv.take<uint32_t>(n_tiles);
+  const uint64_t o_e0 = cv.take<uint32_t>(n_tiles);
   const uint64_t o_lut = cv.take<uint8_t>(256);
   MAGOT_HIP_TRY(hipMalloc(&o->arena, cv.used));
   char* base = static_cast<char*>(o->arena);
-  o->noff = reinterpret_cast<const uint64_t*>(base + o_off);
-  o->soff = reinterpret_cast<const uint64_t*>(base + o_soff);
+  auto up = [&](uint64_t off, const void* src, uint64_t bytes) {
+    return bytes ? hipMemcpy(base + off, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
+  };
+  MAGOT_HIP_TRY(up(o_off, p->nuc_off.data(), (o->n_rec + 1) * 8));
+  MAGOT_HIP_TRY(up(o_soff, o->host_soff.data(), (6 * o->n_rec + 1) * 8));
+  MAGOT_HIP_TRY(up(o_rows, rows.data(), rows.size() * 8));
+  MAGOT_HIP_TRY(up(o_t0, tiles.t0.data(), (n_tiles + 1) * 8));
+  MAGOT_HIP_TRY(up(o_r0, tiles.r0.data(), n_tiles * 4));
+  MAGOT_HIP_TRY(up(o_e0, tiles.e0.data(), n_tiles * 4));
+  MAGOT_HIP_TRY(up(o_lut, tables, 256));
   o->out = reinterpret_cast<uint8_t*>(base + o_out);
-  MAGOT_HIP_TRY(hipMemcpy(base + o_off, p->nuc_off.data(), (o->n_rec + 1) * 8,
-                          hipMemcpyHostToDevice));
-  MAGOT_HIP_TRY(hipMemcpy(base + o_soff, o->host_soff.data(), (6 * o->n_rec + 1) * 8,
-                          hipMemcpyHostToDevice));
-  o->tile_r0 = reinterpret_cast<uint32_t*>(base + o_wj);
-  o->tables = reinterpret_cast<uint8_t*>(base + o_lut);
-  MAGOT_HIP_TRY(hipMemcpy(o->tables, tables, 256, hipMemcpyHostToDevice));
-  launch_orf6_index(o->noff, o->n_rec, o->tile_r0, ctx->stream);
-  MAGOT_HIP_TRY(hipGetLastError());
-  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  Orf6Args& a = o->args;
+  a.nib = p->args.nib;
+  a.nib_words = p->args.span / 4;  // forward + reverse planes, 8 bases per word
+  a.rows = reinterpret_cast<const uint64_t*>(base + o_rows);
+  a.n_rows = ne;
+  a.noff = reinterpret_cast<const uint64_t*>(base + o_off);
+  a.n_rec = o->n_rec;
+  a.total = total_nuc;
+  a.soff = reinterpret_cast<const uint64_t*>(base + o_soff);
+  a.tile_t0 = reinterpret_cast<const uint64_t*>(base + o_t0);
+  a.tile_r0 = reinterpret_cast<const uint32_t*>(base + o_r0);
+  a.tile_e0 = reinterpret_cast<const uint32_t*>(base + o_e0);
+  a.n_tiles = n_tiles;
+  a.tables = reinterpret_cast<const uint8_t*>(base + o_lut);
+  a.out = o->out;
   if (total_res) *total_res = o->total;
   *out = o.release();
   return MAGOT_OK;

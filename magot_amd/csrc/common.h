@@ -137,16 +137,39 @@ void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t
                     uint8_t* out, hipStream_t s);
 // Six translations per record for Sequence.get_orfs (orf6_kernel): stream
 // j = 6*record + 2*frame + (strand == '+'), soff = 6*n_rec+1 padded residue
-// offsets; noff = n_rec+1 offsets of the records in nuc (total_nuc bytes,
-// readable up to the next 16-byte boundary).  tile_r0 (orf6_index_words(
-// total_nuc) u32): the record at every tile start, filled once per record
-// table by launch_orf6_index.  tables_dev: 256 bytes from orf6_tables.
-uint64_t orf6_index_words(uint64_t total_nuc);
+// offsets; noff = n_rec+1 offsets of the records in the concatenation.
+// The records are either bytes (nuc, readable up to the next 16-byte
+// boundary) or gathered from the genome plane through interval rows
+// {unified anchor, start} (n_rows + a sentinel row {0, total}): base P of
+// the concatenation is unified coordinate anchor + P of its interval.
+// Tiles (orf6_plan_tiles): t0 = n_tiles+1 starts, r0 = record holding each
+// start, e0 = interval holding each staged window's first base.
+constexpr uint32_t kOrf6RowCap = 123;  // intervals per staged window
+struct Orf6Args {
+  const uint8_t* nuc;
+  const uint32_t* nib;
+  uint64_t nib_words;  // both planes
+  const uint64_t* rows;
+  uint64_t n_rows;
+  const uint64_t* noff;
+  uint64_t n_rec;
+  uint64_t total;
+  const uint64_t* soff;
+  const uint64_t* tile_t0;
+  const uint32_t* tile_r0;
+  const uint32_t* tile_e0;
+  uint64_t n_tiles;
+  const uint8_t* tables;  // 256 bytes from orf6_tables
+  uint8_t* out;
+};
+struct Orf6Tiles {
+  std::vector<uint64_t> t0;
+  std::vector<uint32_t> r0, e0;
+};
 void orf6_tables(const uint8_t lut64[64], uint8_t out[256]);
-void launch_orf6_index(const uint64_t* noff, uint64_t n_rec, uint32_t* tile_r0, hipStream_t s);
-void launch_orf6(const uint8_t* nuc, const uint64_t* noff, uint64_t n_rec, uint64_t total_nuc,
-                 const uint64_t* soff, const uint32_t* tile_r0, const uint8_t* tables_dev,
-                 uint8_t* out, hipStream_t s);
+void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_start,
+                     uint64_t n_rows, Orf6Tiles* out);
+void launch_orf6(const Orf6Args& a, bool genome, hipStream_t s);
 void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const int32_t* frames,
                       const uint8_t* strands, const uint64_t* pep_off, uint64_t total_pep,
                       const uint32_t* lut16, uint8_t* out, hipStream_t s);

@@ -3,6 +3,8 @@
 //   translate_kernel -- Sequence.translate           genome.py:795-822
 // Both are output-stationary: a lane owns 16 aligned output bytes, finds its
 // record by binary search over the offset table and reads its inputs from L2.
+#include <algorithm>
+
 #include "common.h"
 
 namespace magot {
@@ -163,26 +165,15 @@ __global__ __launch_bounds__(kOpsThreads) void translate_kernel(
 // streams.  Each staged record byte feeds ~2 output bytes, so the kernel
 // streams the nucleotides once and writes the residues once.
 // ---------------------------------------------------------------------------
-constexpr int64_t kOrfTile = 3968;  // bases per wave tile: + halo and alignment = 256 x 16 B
-constexpr int kOrfVecs = 256;       // staged 16-byte vectors per wave
-constexpr int kOrfBatch = 16;       // records per segment batch
+constexpr uint64_t kOrfTile = 3968;  // max bases per wave tile: + halo and alignment = 256 x 16 B
+constexpr int kOrfVecs = 256;        // staged 16-byte vectors per wave
+constexpr int kOrfBatch = 10;        // records per segment batch: one (record, stream) per lane
 constexpr int kOrfSegs = 6 * kOrfBatch;
-constexpr int kOrfRankWords = 128;  // chunk bitmap: a batch owns < 4096 chunks
+constexpr int kOrfRankWords = 128;   // chunk bitmap: a batch owns < 4096 chunks
 
 // real codons of frame f in a record of L bases (0 when translate() is None)
 __device__ __host__ __forceinline__ uint64_t orf_count(uint64_t L, uint32_t f) {
   return (L > 2 + f && L >= 2 * f + 3) ? (L - 2 * f) / 3 : 0;
-}
-
-// tile_r0[t] = the record holding base t * kOrfTile of the concatenation.
-__global__ __launch_bounds__(kOpsThreads) void orf6_index_kernel(const uint64_t* __restrict__ noff,
-                                                                uint64_t n_rec,
-                                                                uint32_t* __restrict__ tile_r0) {
-  const uint64_t r = (uint64_t)blockIdx.x * kOpsThreads + threadIdx.x;
-  if (r >= n_rec) return;
-  const uint64_t a = noff[r], b = noff[r + 1];
-  for (uint64_t t = (a + kOrfTile - 1) / kOrfTile; (uint64_t)t * kOrfTile < b; ++t)
-    tile_r0[t] = (uint32_t)r;
 }
 
 // A run of output chunks of one stream, rebased so that the wave-wide chunk
@@ -199,84 +190,185 @@ __device__ __forceinline__ uint64_t div48(uint64_t v) {
   return v < (1ull << 32) ? (uint64_t)((uint32_t)v / 48u) : v / 48;
 }
 
-__global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
-    const uint8_t* __restrict__ nuc, const uint64_t* __restrict__ noff, uint64_t n_rec,
-    uint64_t total, const uint64_t* __restrict__ soff, const uint32_t* __restrict__ tile_r0,
-    const uint8_t* __restrict__ tables, uint64_t n_tiles, uint8_t* __restrict__ out) {
+__device__ __forceinline__ uint32_t funnel4(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return __builtin_amdgcn_alignbit(hi, lo, sh);
+}
+
+// Eight nibbles (code | lower << 2 | exception << 3) -> two words of
+// e-bytes (code | exception << 6), one base per byte.
+__device__ __forceinline__ void nibbles_to_e(uint32_t x, uint32_t& e0, uint32_t& e1) {
+  const uint32_t lo = x & 0x0F0F0F0Fu;         // nibbles 0 2 4 6
+  const uint32_t hi = (x >> 4) & 0x0F0F0F0Fu;  // nibbles 1 3 5 7
+  const uint32_t s0 = __builtin_amdgcn_perm(hi, lo, 0x05010400u);
+  const uint32_t s1 = __builtin_amdgcn_perm(hi, lo, 0x07030602u);
+  e0 = (s0 & 0x03030303u) | ((s0 & 0x08080808u) << 3);
+  e1 = (s1 & 0x03030303u) | ((s1 & 0x08080808u) << 3);
+}
+
+// cidx bytes of 16 positions from their e-bytes and the next two.
+__device__ __forceinline__ uint4 codon_indices(const uint32_t e[5]) {
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t e1 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 1);
+    const uint32_t e2 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 2);
+    o[j] = (e[j] & 0x03030303u) | ((e1 & 0x03030303u) << 2) | ((e2 & 0x03030303u) << 4) |
+           ((e[j] | e1 | e2) & 0x40404040u);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// kGenome = false: the records are bytes in a.nuc (Sequence.get_orfs batch).
+// kGenome = true:  the records are gathered from the genome's nibble plane
+//                  through the plan's intervals (a.rows), never written out
+//                  as nucleotides (C5: extraction fused with translation).
+template <bool kGenome>
+__global__ __launch_bounds__(kOpsThreads) void orf6_kernel(Orf6Args a) {
   __shared__ uint8_t s_tbl[256];   // residue of cidx: [0,128) '+', [128,256) '-'
   __shared__ uint8_t s_code[256];  // byte -> 2-bit code, or 0x40 when not ACGTacgt
   __shared__ uint4 s_stage[kOpsThreads / 64][kOrfVecs];
-  __shared__ OrfSeg s_seg[kOpsThreads / 64][kOrfSegs];
-  __shared__ uint32_t s_bm[kOpsThreads / 64][kOrfRankWords];
-  __shared__ uint32_t s_pre[kOpsThreads / 64][kOrfRankWords];
+  // per wave: the staging window's interval rows, then (same bytes) the
+  // segment table and the chunk bitmap with its prefix counts
+  constexpr int kScratch = 2 * (kOrf6RowCap + 1);
+  static_assert(kScratch * 8 >= kOrfSegs * 16 + 2 * kOrfRankWords * 4, "scratch too small");
+  __shared__ uint64_t s_scratch[kOpsThreads / 64][kScratch];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  s_tbl[threadIdx.x] = tables[threadIdx.x];
+  s_tbl[threadIdx.x] = a.tables[threadIdx.x];
   {
     const uint32_t c = code_of(threadIdx.x);
     s_code[threadIdx.x] = (uint8_t)(c < 4 ? c : 0x40u);
   }
   __syncthreads();
   const uint64_t tile = (uint64_t)blockIdx.x * (kOpsThreads / 64) + wave;
-  if (tile >= n_tiles) return;  // wave-uniform
-  const uint64_t T0 = tile * kOrfTile, T1 = min(T0 + kOrfTile, total);
+  if (tile >= a.n_tiles) return;  // wave-uniform
+  const uint64_t T0 = a.tile_t0[tile], T1 = a.tile_t0[tile + 1];
   const uint64_t W0 = (T0 >= 48 ? T0 - 48 : 0) & ~15ull;
-  const uint64_t WE = min(T1 + 50, total);
+  const uint64_t WE = min(T1 + 50, a.total);
   const uint32_t nvec = (uint32_t)((WE - W0 + 15) / 16);
-  // raw staging: all loads in flight at once, stored to LDS when they land;
-  // converted to codon indices in place after the record reads
   constexpr int kPer = kOrfVecs / 64;
-  {
+  // the first record batch's offsets, in flight with the staging loads
+  const uint32_t my_s = (uint32_t)lane % 6u, my_f = my_s >> 1;
+  const bool my_plus = my_s & 1u;
+  uint64_t rb = a.tile_r0[tile];
+  uint64_t nb = 0, L = 0;
+  bool rec = lane < kOrfSegs && rb + (uint64_t)lane / 6u < a.n_rec;
+  if (rec) {
+    nb = a.noff[rb + (uint64_t)lane / 6u];
+    L = a.noff[rb + (uint64_t)lane / 6u + 1] - nb;
+  }
+  if (!kGenome) {
+    // raw bytes: all loads in flight at once, to LDS when they land
     uint4 v[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t t = min((uint32_t)(lane + 64 * k), nvec - 1);
-      v[k] = *reinterpret_cast<const uint4*>(nuc + W0 + 16 * (uint64_t)t);
+      v[k] = *reinterpret_cast<const uint4*>(a.nuc + W0 + 16 * (uint64_t)t);
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) s_stage[wave][lane + 64 * k] = v[k];
+  } else {
+    // the window's intervals (<= kOrf6RowCap, host-planned): {anchor, start}
+    uint64_t* const row = s_scratch[wave];
+    const uint64_t e0 = a.tile_e0[tile];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t j = min(e0 + (uint64_t)(lane + 64 * h), a.n_rows);  // sentinel row n_rows
+      if (lane + 64 * h <= kOrf6RowCap) {
+        row[2 * (lane + 64 * h)] = a.rows[2 * j];
+        row[2 * (lane + 64 * h) + 1] = a.rows[2 * j + 1];
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t m = kOrf6RowCap;  // rows with start < WE
+    {
+      uint32_t lo = 0, hi = kOrf6RowCap + 1;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (row[2 * mid + 1] < WE) lo = mid;
+        else hi = mid;
+      }
+      m = lo + 1;
+    }
+    // e-bytes of vector t: its first interval by binary search and that
+    // interval's plane words for all four vectors in flight at once; the
+    // rest of a vector that crosses into later intervals afterwards
+    uint32_t iv[kPer], wv[kPer][3];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint64_t P = W0 + 16 * (uint64_t)(lane + 64 * k);
+      uint32_t i = 0, hi = m;
+      while (hi - i > 1) {
+        const uint32_t mid = (i + hi) >> 1;
+        if (row[2 * mid + 1] <= P) i = mid;
+        else hi = mid;
+      }
+      iv[k] = i;
+      const uint64_t u = row[2 * i] + P;  // chunk byte j <- unified base u + j
+      const uint32_t* w = a.nib + min(u >> 3, a.nib_words - 3);  // clamp: never off the plane
+      wv[k][0] = w[0];
+      wv[k][1] = w[1];
+      wv[k][2] = w[2];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t t = lane + 64 * k;
+      const uint64_t P = W0 + 16 * (uint64_t)t;
+      const uint64_t end = min(P + 16, WE);
+      uint32_t i = iv[k];
+      uint64_t u = row[2 * i] + P;
+      uint32_t sh = 4u * (uint32_t)(u & 7);
+      uint32_t x0 = funnel4(wv[k][1], wv[k][0], sh), x1 = funnel4(wv[k][2], wv[k][1], sh);
+      uint64_t pos = min(row[2 * i + 3], end);  // first interval ends here
+      while (pos < end) {  // later intervals of this vector
+        ++i;
+        u = row[2 * i] + P;
+        const uint32_t* w = a.nib + min(u >> 3, a.nib_words - 3);
+        sh = 4u * (uint32_t)(u & 7);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        const uint32_t j0 = (uint32_t)(pos - P);
+        const uint32_t n = (uint32_t)(min(row[2 * i + 3], end) - pos);
+        const uint64_t msk = (n >= 16 ? ~0ull : ((1ull << (4 * n)) - 1ull)) << (4 * j0);
+        x0 = (funnel4(w1, w0, sh) & (uint32_t)msk) | (x0 & ~(uint32_t)msk);
+        x1 = (funnel4(w2, w1, sh) & (uint32_t)(msk >> 32)) | (x1 & ~(uint32_t)(msk >> 32));
+        pos += n;
+      }
+      uint32_t e[4];
+      nibbles_to_e(x0, e[0], e[1]);
+      nibbles_to_e(x1, e[2], e[3]);
+      s_stage[wave][t] = make_uint4(e[0], e[1], e[2], e[3]);
+    }
   }
   const uint8_t* const stage = reinterpret_cast<const uint8_t*>(s_stage[wave]);
-  OrfSeg* const seg = s_seg[wave];
-  uint32_t* const bm = s_bm[wave];
-  uint32_t* const pre = s_pre[wave];
+  OrfSeg* const seg = reinterpret_cast<OrfSeg*>(s_scratch[wave]);
+  uint32_t* const bm = reinterpret_cast<uint32_t*>(s_scratch[wave] + 2 * kOrfSegs);
+  uint32_t* const pre = bm + kOrfRankWords;
   bool staged = false;
-  for (uint64_t rb = tile_r0[tile];; rb += kOrfBatch) {
-    // ---- the batch's segments: lane < kOrfBatch owns record rb + lane
-    const uint64_t r = rb + (uint64_t)lane;
-    uint64_t nb = 0, L = 0;
-    const bool rec = lane < kOrfBatch && r < n_rec;
-    if (rec) {
-      nb = noff[r];
-      L = noff[r + 1] - nb;
+  for (;; rb += kOrfBatch) {
+    // ---- the batch's segments: lane 6i + s owns stream s of record rb + i
+    const uint64_t r = rb + (uint64_t)lane / 6u;
+    if (staged) {
+      rec = lane < kOrfSegs && r < a.n_rec;
+      nb = rec ? a.noff[r] : 0;
+      L = rec ? a.noff[r + 1] - nb : 0;
     }
-    const bool mine = rec && nb < T1;
-    uint32_t cnt[6], lo_c[6], nres_c[6];
-    uint32_t lane_total = 0, lane_segs = 0;
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const uint32_t f = (uint32_t)s >> 1;
-      const uint64_t nres = mine ? orf_count(L, f) : 0;
-      const uint64_t nch = (nres + 15) / 16;
-      uint64_t lo, hi;
-      if (s & 1) {  // '+': chunk c's first codon starts at x0 + 48c
-        const uint64_t x0 = nb + 2 * f;
+    const uint64_t nres = rec && nb < T1 ? orf_count(L, my_f) : 0;
+    uint64_t lo = 0, hi = 0;
+    if (nres) {
+      if (my_plus) {  // '+': chunk c's first codon starts at x0 + 48c
+        const uint64_t x0 = nb + 2 * my_f;
         lo = T0 > x0 ? div48(T0 - x0 + 47) : 0;
         hi = T1 > x0 ? div48(T1 - x0 + 47) : 0;
       } else {  // '-': chunk c's first codon (read backwards) lies at x0 - 48c
-        const uint64_t x0 = nb + L - 3 - 2 * f;  // only used when nres > 0
+        const uint64_t x0 = nb + L - 3 - 2 * my_f;
         lo = x0 >= T1 ? div48(x0 - T1) + 1 : 0;
         hi = x0 >= T0 ? div48(x0 - T0) + 1 : 0;
       }
-      hi = nres ? min(hi, nch) : 0;
+      hi = min(hi, (nres + 15) / 16);
       lo = min(lo, hi);
-      cnt[s] = (uint32_t)(hi - lo);
-      lo_c[s] = (uint32_t)lo;
-      nres_c[s] = (uint32_t)nres;
-      lane_total += cnt[s];
-      lane_segs += cnt[s] != 0;
     }
+    const uint32_t cnt = (uint32_t)(hi - lo);
     // wave-inclusive scans: chunk starts and compacted segment slots
-    uint32_t incl = lane_total, incl_s = lane_segs;
+    uint32_t incl = cnt, incl_s = cnt != 0;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(incl, d, 64), z = __shfl_up(incl_s, d, 64);
@@ -287,8 +379,8 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
     }
     const uint32_t n_chunks = __shfl(incl, 63, 64);
     // does the next batch still start inside the tile?
-    const bool more = __shfl((int)(rec && nb + L < T1), kOrfBatch - 1, 64) &&
-                      rb + kOrfBatch < n_rec;
+    const bool more = __shfl((int)(rec && nb + L < T1), kOrfSegs - 1, 64) &&
+                      rb + kOrfBatch < a.n_rec;
     bm[lane] = 0u;
     bm[lane + 64] = 0u;
     if (!staged) {  // cidx[p] = c[p] | c[p+1] << 2 | c[p+2] << 4 | invalid << 6
@@ -298,62 +390,53 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
       for (int k = 0; k < kPer; ++k) {
         const uint32_t t = lane + 64 * k;
         const uint4 raw = s_stage[wave][t];
-        const uint32_t nxt = reinterpret_cast<const uint32_t*>(s_stage[wave])[4 * min(t + 1, (uint32_t)kOrfVecs - 1)];
+        const uint32_t nxt =
+            reinterpret_cast<const uint32_t*>(s_stage[wave])[4 * min(t + 1, (uint32_t)kOrfVecs - 1)];
         __builtin_amdgcn_wave_barrier();
         const uint32_t w[5] = {raw.x, raw.y, raw.z, raw.w, nxt};
         uint32_t e[5];
+        if (kGenome) {
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const uint32_t x = w[j];
-          e[j] = (uint32_t)s_code[x & 0xFFu] | ((uint32_t)s_code[(x >> 8) & 0xFFu] << 8);
-          if (j < 4)
-            e[j] |= ((uint32_t)s_code[(x >> 16) & 0xFFu] << 16) | ((uint32_t)s_code[x >> 24] << 24);
-        }
-        uint32_t o[4];
+          for (int j = 0; j < 5; ++j) e[j] = w[j];
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t e1 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 1);
-          const uint32_t e2 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 2);
-          o[j] = (e[j] & 0x03030303u) | ((e1 & 0x03030303u) << 2) | ((e2 & 0x03030303u) << 4) |
-                 ((e[j] | e1 | e2) & 0x40404040u);
+          for (int j = 0; j < 5; ++j) {
+            const uint32_t x = w[j];
+            e[j] = (uint32_t)s_code[x & 0xFFu] | ((uint32_t)s_code[(x >> 8) & 0xFFu] << 8);
+            if (j < 4)
+              e[j] |= ((uint32_t)s_code[(x >> 16) & 0xFFu] << 16) |
+                      ((uint32_t)s_code[x >> 24] << 24);
+          }
         }
-        s_stage[wave][t] = make_uint4(o[0], o[1], o[2], o[3]);
+        s_stage[wave][t] = codon_indices(e);
         __builtin_amdgcn_wave_barrier();
       }
       staged = true;
     }
     __builtin_amdgcn_wave_barrier();
-    if (lane < kOrfBatch) {
-      uint32_t start = incl - lane_total, slot = incl_s - lane_segs;
-#pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        if (!cnt[s]) continue;
-        const uint32_t f = (uint32_t)s >> 1;
-        const bool plus = s & 1;
-        const uint64_t lo = lo_c[s];
-        const int64_t p = plus ? (int64_t)(nb + 2 * f + 48 * lo)
-                               : (int64_t)(nb + L - 3 - 2 * f - 48 * lo);
-        OrfSeg g;
-        g.out0 = soff[6 * r + (uint64_t)s] + 16 * lo - 16 * (uint64_t)start;
-        g.p0 = (int32_t)(p - (int64_t)W0 + (plus ? -48 : 48) * (int64_t)start);
-        const int32_t rem = (int32_t)(nres_c[s] - 16 * lo) + 16 * (int32_t)start;
-        g.rem0 = plus ? rem : -rem;
-        seg[slot++] = g;
-        atomicOr(&bm[start >> 5], 1u << (start & 31));
-        start += cnt[s];
-      }
+    if (cnt) {
+      const uint32_t start = incl - cnt;
+      const int64_t p = my_plus ? (int64_t)(nb + 2 * my_f + 48 * lo)
+                                : (int64_t)(nb + L - 3 - 2 * my_f - 48 * lo);
+      OrfSeg g;
+      g.out0 = a.soff[6 * r + my_s] + 16 * lo - 16 * (uint64_t)start;
+      g.p0 = (int32_t)(p - (int64_t)W0 + (my_plus ? -48 : 48) * (int64_t)start);
+      const int32_t rem = (int32_t)(nres - 16 * lo) + 16 * (int32_t)start;
+      g.rem0 = my_plus ? rem : -rem;
+      seg[incl_s - 1] = g;
+      atomicOr(&bm[start >> 5], 1u << (start & 31));
     }
     __builtin_amdgcn_wave_barrier();
     {  // pre[w] = segment starts in words before w
-      const uint32_t a = __popc(bm[2 * lane]), b = __popc(bm[2 * lane + 1]);
-      uint32_t x = a + b;
+      const uint32_t x0 = __popc(bm[2 * lane]), x1 = __popc(bm[2 * lane + 1]);
+      uint32_t x = x0 + x1;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
       }
-      pre[2 * lane] = x - a - b;
-      pre[2 * lane + 1] = x - b;
+      pre[2 * lane] = x - x0 - x1;
+      pre[2 * lane + 1] = x - x1;
     }
     __builtin_amdgcn_wave_barrier();
     // ---- the batch's chunks, 64 at a time
@@ -377,18 +460,15 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
         o[2] = __builtin_amdgcn_perm(0u, t1, 0x00010203u);
         o[3] = __builtin_amdgcn_perm(0u, t0, 0x00010203u);
       }
-      if (rem < 16) {  // stream end: residues past it repeat the last one
-        const uint32_t last = (uint32_t)rem - 1;
-        const uint32_t lw = last >> 2 == 0 ? o[0] : last >> 2 == 1 ? o[1] : last >> 2 == 2 ? o[2] : o[3];
-        const uint32_t fill = ((lw >> (8 * (last & 3))) & 0xFFu) * 0x01010101u;
+      if (rem < 16) {  // stream end: the padding bytes are zero
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int32_t keep = min(max(rem - 4 * j, 0), 4);  // bytes of word j kept
-          const uint32_t mask = keep >= 4 ? 0xFFFFFFFFu : ((1u << (8 * keep)) - 1u);
-          o[j] = (o[j] & mask) | (fill & ~mask);
+          const uint32_t drop = (uint32_t)min(max(4 * j + 4 - rem, 0), 4);  // bytes of word j
+          o[j] &= (uint32_t)(0xFFFFFFFFull >> (8 * drop));
         }
       }
-      *reinterpret_cast<uint4*>(out + g.out0 + 16 * (uint64_t)q) = make_uint4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<uint4*>(a.out + g.out0 + 16 * (uint64_t)q) =
+          make_uint4(o[0], o[1], o[2], o[3]);
     }
     if (!more) break;
     __builtin_amdgcn_wave_barrier();  // segment tables are rewritten
@@ -396,10 +476,6 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(
 }
 
 }  // namespace
-
-uint64_t orf6_index_words(uint64_t total_nuc) {
-  return (total_nuc + kOrfTile - 1) / kOrfTile + 1;
-}
 
 void orf6_tables(const uint8_t lut64[64], uint8_t out[256]) {
   // '+': cidx = c0 | c1 << 2 | c2 << 4 indexes the library directly;
@@ -412,20 +488,40 @@ void orf6_tables(const uint8_t lut64[64], uint8_t out[256]) {
   }
 }
 
-void launch_orf6_index(const uint64_t* noff, uint64_t n_rec, uint32_t* tile_r0, hipStream_t s) {
-  if (n_rec == 0) return;
-  hipLaunchKernelGGL(orf6_index_kernel, dim3((uint32_t)((n_rec + kOpsThreads - 1) / kOpsThreads)),
-                     dim3(kOpsThreads), 0, s, noff, n_rec, tile_r0);
+void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_start,
+                     uint64_t n_rows, Orf6Tiles* out) {
+  const uint64_t total = n_rec ? noff[n_rec] : 0;
+  out->t0.clear();
+  out->r0.clear();
+  out->e0.clear();
+  uint64_t r = 0, e = 0;
+  for (uint64_t T = 0; T < total;) {
+    const uint64_t W0 = (T >= 48 ? T - 48 : 0) & ~15ull;
+    while (r + 1 < n_rec && noff[r + 1] <= T) ++r;  // the record holding base T
+    uint64_t T1 = std::min(T + kOrfTile, total);
+    if (row_start) {
+      while (e + 1 < n_rows && row_start[e + 1] <= W0) ++e;  // the interval holding W0
+      // at most kOrf6RowCap intervals may start before the staged window ends
+      if (e + kOrf6RowCap < n_rows) {
+        const uint64_t cap = row_start[e + kOrf6RowCap];
+        if (T1 + 50 > cap) T1 = std::max(T + 1, cap - 50);
+      }
+      out->e0.push_back((uint32_t)e);
+    }
+    out->t0.push_back(T);
+    out->r0.push_back((uint32_t)r);
+    T = T1;
+  }
+  out->t0.push_back(total);
 }
 
-void launch_orf6(const uint8_t* nuc, const uint64_t* noff, uint64_t n_rec, uint64_t total_nuc,
-                 const uint64_t* soff, const uint32_t* tile_r0, const uint8_t* tables_dev,
-                 uint8_t* out, hipStream_t s) {
-  if (total_nuc == 0 || n_rec == 0) return;
-  const uint64_t n_tiles = (total_nuc + kOrfTile - 1) / kOrfTile;
-  const uint64_t blocks = (n_tiles + kOpsThreads / 64 - 1) / (kOpsThreads / 64);
-  hipLaunchKernelGGL(orf6_kernel, dim3((uint32_t)blocks), dim3(kOpsThreads), 0, s, nuc, noff,
-                     n_rec, total_nuc, soff, tile_r0, tables_dev, n_tiles, out);
+void launch_orf6(const Orf6Args& a, bool genome, hipStream_t s) {
+  if (a.n_tiles == 0) return;
+  const uint64_t blocks = (a.n_tiles + kOpsThreads / 64 - 1) / (kOpsThreads / 64);
+  if (genome)
+    hipLaunchKernelGGL(orf6_kernel<true>, dim3((uint32_t)blocks), dim3(kOpsThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(orf6_kernel<false>, dim3((uint32_t)blocks), dim3(kOpsThreads), 0, s, a);
 }
 
 void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t total,

@@ -422,7 +422,9 @@ def orf6_batch(seqs, lut64=None, ctx=None):
 
 class Orf6Plan(object):
     """Six-frame translation of an ExtractionPlan's records, in HBM
-    (magot_plan_orf6): BASELINE configs[4] (C5)."""
+    (magot_plan_orf6): BASELINE configs[4] (C5).  The kernel gathers the
+    records from the packed genome itself (the plan's nucleotide output is
+    neither needed nor read)."""
 
     def __init__(self, plan, lut64=None):
         self.plan = plan

@@ -402,6 +402,7 @@ def test_orf6_over_extraction_plan_vs_oracle():
         for k in range(6):
             j = 6 * r + k
             assert int(soff[j]) % 16 == 0
+            assert not out[int(soff[j] + slen[j]):int(soff[j + 1])].any()  # zero padding
             t = raw[int(soff[j]):int(soff[j] + slen[j])]
             if k < 2 and t[:1] == 'X':
                 t = t[1:]
@@ -409,6 +410,47 @@ def test_orf6_over_extraction_plan_vs_oracle():
                 assert t == ''
             else:
                 assert t == want[k], (r, k)
+    o6.close()
+    plan.close()
+    dev.close()
+
+
+def test_orf6_fused_gather_tiny_intervals_vs_oracle():
+    """The fused gather over 1-6 base intervals on both strands (many
+    intervals per 16-base vector, windows shortened to the interval cap) and
+    long records spanning several tiles."""
+    rng = np.random.default_rng(53)
+    w = synth.make('small', seed=53, genome_bases=300_000, n_tx=10, iupac_rate=5e-3)
+    dev = engine.DeviceGenome(w.contigs())
+    lens = [len(s) for _, s in w.contigs()]
+    rows, txs = [], []
+    for t in range(700):
+        n = int(rng.integers(1, 40)) if t % 50 else 3000  # a few records of ~10 kb
+        b = len(rows)
+        for _ in range(n):
+            c = int(rng.integers(0, len(lens)))
+            ln = int(rng.integers(0, 7)) if t % 3 else int(rng.integers(1, 9))
+            st = int(rng.integers(0, lens[c] - ln))
+            rows.append(((st | (1 << 63)) if rng.integers(0, 2) else st, c, ln))
+        txs.append((b, n, 0))
+    ex = np.array(rows, dtype=engine.EXON_DTYPE)
+    tx = np.array(txs, dtype=engine.TX_DTYPE)
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    nuc, noff, _, _ = plan.run()
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    raw = out.tobytes().decode('latin-1')
+    for r in range(len(tx)):
+        s = nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1')
+        want = _oracle_six(s)
+        for k in range(6):
+            j = 6 * r + k
+            assert not out[int(soff[j] + slen[j]):int(soff[j + 1])].any()
+            t = raw[int(soff[j]):int(soff[j] + slen[j])]
+            if k < 2 and t[:1] == 'X':
+                t = t[1:]
+            assert t == (want[k] or ''), (r, k)
     o6.close()
     plan.close()
     dev.close()
