@@ -218,12 +218,49 @@ __device__ __forceinline__ uint4 codon_indices(const uint32_t e[5]) {
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// One 16-residue chunk per lane.  kMode 0: every lane '+', 1: every lane
+// '-' (wave-uniform: table offsets fold into the LDS immediates), 2: mixed.
+template <int kMode>
+__device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* stage,
+                                           const uint8_t* tbl, const OrfSeg* seg,
+                                           const uint32_t* bm, const uint32_t* pre, uint32_t q,
+                                           uint32_t n_chunks) {
+  if (q >= n_chunks) return;
+  const uint32_t wq = q >> 5;
+  const uint32_t rank = pre[wq] + __popc(bm[wq] & (0xFFFFFFFFu >> (31 - (q & 31))));
+  const OrfSeg g = seg[rank - 1];
+  const bool minus = kMode == 1 ? true : kMode == 0 ? false : g.rem0 < 0;
+  const int32_t rem = (minus ? -g.rem0 : g.rem0) - 16 * (int32_t)q;
+  const int32_t p = g.p0 + (minus ? -48 : 48) * (int32_t)q;
+  // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed below)
+  const uint8_t* const src = stage + (minus ? p - 45 : p);
+  const uint8_t* const tb = kMode == 2 ? tbl + (minus ? 128 : 0) : tbl + (kMode == 1 ? 128 : 0);
+  uint32_t o[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i >> 2] |= (uint32_t)tb[src[3 * i]] << (8 * (i & 3));
+  if (minus) {
+    const uint32_t t0 = o[0], t1 = o[1];
+    o[0] = __builtin_amdgcn_perm(0u, o[3], 0x00010203u);
+    o[1] = __builtin_amdgcn_perm(0u, o[2], 0x00010203u);
+    o[2] = __builtin_amdgcn_perm(0u, t1, 0x00010203u);
+    o[3] = __builtin_amdgcn_perm(0u, t0, 0x00010203u);
+  }
+  if (rem < 16) {  // stream end: the padding bytes are zero
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t drop = (uint32_t)min(max(4 * j + 4 - rem, 0), 4);  // bytes of word j
+      o[j] &= (uint32_t)(0xFFFFFFFFull >> (8 * drop));
+    }
+  }
+  *reinterpret_cast<uint4*>(a.out + g.out0 + 16 * (uint64_t)q) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // kGenome = false: the records are bytes in a.nuc (Sequence.get_orfs batch).
 // kGenome = true:  the records are gathered from the genome's nibble plane
 //                  through the plan's intervals (a.rows), never written out
 //                  as nucleotides (C5: extraction fused with translation).
 template <bool kGenome>
-__global__ __launch_bounds__(kOpsThreads) void orf6_kernel(Orf6Args a) {
+__global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   __shared__ uint8_t s_tbl[256];   // residue of cidx: [0,128) '+', [128,256) '-'
   __shared__ uint8_t s_code[256];  // byte -> 2-bit code, or 0x40 when not ACGTacgt
   __shared__ uint4 s_stage[kOpsThreads / 64][kOrfVecs];
@@ -246,15 +283,20 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(Orf6Args a) {
   const uint64_t WE = min(T1 + 50, a.total);
   const uint32_t nvec = (uint32_t)((WE - W0 + 15) / 16);
   constexpr int kPer = kOrfVecs / 64;
+  // lanes [0, 30): the '-' streams of the batch's 10 records, [30, 60): the
+  // '+' streams, so the chunks of each strand are contiguous in q and most
+  // chunk iterations are strand-uniform
+  const uint32_t my_k = (uint32_t)(lane < kOrfSegs / 2 ? lane : lane - kOrfSegs / 2);
+  const uint32_t my_rec = my_k / 3u, my_f = my_k % 3u;
+  const bool my_plus = lane >= kOrfSegs / 2;
+  const uint32_t my_s = 2u * my_f + (my_plus ? 1u : 0u);
   // the first record batch's offsets, in flight with the staging loads
-  const uint32_t my_s = (uint32_t)lane % 6u, my_f = my_s >> 1;
-  const bool my_plus = my_s & 1u;
   uint64_t rb = a.tile_r0[tile];
   uint64_t nb = 0, L = 0;
-  bool rec = lane < kOrfSegs && rb + (uint64_t)lane / 6u < a.n_rec;
+  bool rec = lane < kOrfSegs && rb + my_rec < a.n_rec;
   if (rec) {
-    nb = a.noff[rb + (uint64_t)lane / 6u];
-    L = a.noff[rb + (uint64_t)lane / 6u + 1] - nb;
+    nb = a.noff[rb + my_rec];
+    L = a.noff[rb + my_rec + 1] - nb;
   }
   if (!kGenome) {
     // raw bytes: all loads in flight at once, to LDS when they land
@@ -269,41 +311,57 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(Orf6Args a) {
   } else {
     // the window's intervals (<= kOrf6RowCap, host-planned): {anchor, start}
     uint64_t* const row = s_scratch[wave];
+    uint32_t* const cnt = reinterpret_cast<uint32_t*>(s_stage[wave]);  // 256 counters, then map
     const uint64_t e0 = a.tile_e0[tile];
+    uint64_t rs[2];
+    bool in[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint64_t j = min(e0 + (uint64_t)(lane + 64 * h), a.n_rows);  // sentinel row n_rows
-      if (lane + 64 * h <= kOrf6RowCap) {
-        row[2 * (lane + 64 * h)] = a.rows[2 * j];
-        row[2 * (lane + 64 * h) + 1] = a.rows[2 * j + 1];
+      const uint32_t jj = lane + 64 * h;
+      const uint64_t j = min(e0 + (uint64_t)jj, a.n_rows);  // sentinel row n_rows
+      rs[h] = a.rows[2 * j + 1];
+      in[h] = jj <= kOrf6RowCap && rs[h] < WE;
+      if (jj <= kOrf6RowCap) {
+        row[2 * jj] = a.rows[2 * j];
+        row[2 * jj + 1] = rs[h];
+      }
+    }
+    s_stage[wave][lane] = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t m = (uint32_t)(__popcll(__ballot(in[0])) + __popcll(__ballot(in[1])));
+    __builtin_amdgcn_wave_barrier();
+    // first interval of every vector: count interval starts per vector
+    // (a start in (P_v - 16, P_v] counts at vector v), then prefix sums
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (in[h]) {
+        const uint64_t v = rs[h] <= W0 ? 0 : (rs[h] - W0 + 15) >> 4;
+        if (v < (uint64_t)kOrfVecs) atomicAdd(&cnt[v], 1u);
       }
     }
     __builtin_amdgcn_wave_barrier();
-    uint32_t m = kOrf6RowCap;  // rows with start < WE
     {
-      uint32_t lo = 0, hi = kOrf6RowCap + 1;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (row[2 * mid + 1] < WE) lo = mid;
-        else hi = mid;
+      const uint4 c = s_stage[wave][lane];  // vectors 4 lane .. 4 lane + 3
+      const uint32_t c0 = c.x, c1 = c0 + c.y, c2 = c1 + c.z, c3 = c2 + c.w;
+      uint32_t x = c3;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
       }
-      m = lo + 1;
+      const uint32_t base = x - c3 - 1;
+      s_stage[wave][lane] = make_uint4(base + c0, base + c1, base + c2, base + c3);
     }
-    // e-bytes of vector t: its first interval by binary search and that
-    // interval's plane words for all four vectors in flight at once; the
-    // rest of a vector that crosses into later intervals afterwards
+    __builtin_amdgcn_wave_barrier();
+    // e-bytes of vector t: its first interval's plane words for all four
+    // vectors in flight at once; the rest of a vector that crosses into
+    // later intervals afterwards
     uint32_t iv[kPer], wv[kPer][3];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) iv[k] = min(cnt[lane + 64 * k], m - 1);
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint64_t P = W0 + 16 * (uint64_t)(lane + 64 * k);
-      uint32_t i = 0, hi = m;
-      while (hi - i > 1) {
-        const uint32_t mid = (i + hi) >> 1;
-        if (row[2 * mid + 1] <= P) i = mid;
-        else hi = mid;
-      }
-      iv[k] = i;
-      const uint64_t u = row[2 * i] + P;  // chunk byte j <- unified base u + j
+      const uint64_t u = row[2 * iv[k]] + P;  // chunk byte j <- unified base u + j
       const uint32_t* w = a.nib + min(u >> 3, a.nib_words - 3);  // clamp: never off the plane
       wv[k][0] = w[0];
       wv[k][1] = w[1];
@@ -344,8 +402,8 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(Orf6Args a) {
   uint32_t* const pre = bm + kOrfRankWords;
   bool staged = false;
   for (;; rb += kOrfBatch) {
-    // ---- the batch's segments: lane 6i + s owns stream s of record rb + i
-    const uint64_t r = rb + (uint64_t)lane / 6u;
+    // ---- the batch's segments: one (record, stream) per lane
+    const uint64_t r = rb + my_rec;
     if (staged) {
       rec = lane < kOrfSegs && r < a.n_rec;
       nb = rec ? a.noff[r] : 0;
@@ -378,6 +436,7 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(Orf6Args a) {
       }
     }
     const uint32_t n_chunks = __shfl(incl, 63, 64);
+    const uint32_t n_minus = __shfl(incl, kOrfSegs / 2 - 1, 64);  // '-' chunks come first
     // does the next batch still start inside the tile?
     const bool more = __shfl((int)(rec && nb + L < T1), kOrfSegs - 1, 64) &&
                       rb + kOrfBatch < a.n_rec;
@@ -440,35 +499,11 @@ __global__ __launch_bounds__(kOpsThreads) void orf6_kernel(Orf6Args a) {
     }
     __builtin_amdgcn_wave_barrier();
     // ---- the batch's chunks, 64 at a time
-    for (uint32_t q = lane; q < n_chunks; q += 64) {
-      const uint32_t wq = q >> 5;
-      const uint32_t rank = pre[wq] + __popc(bm[wq] & (0xFFFFFFFFu >> (31 - (q & 31))));
-      const OrfSeg g = seg[rank - 1];
-      const bool minus = g.rem0 < 0;
-      const int32_t rem = (minus ? -g.rem0 : g.rem0) - 16 * (int32_t)q;
-      const int32_t p = g.p0 + (minus ? -48 : 48) * (int32_t)q;
-      // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed below)
-      const uint8_t* const src = stage + (minus ? p - 45 : p);
-      const uint8_t* const tb = s_tbl + (minus ? 128 : 0);
-      uint32_t o[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int i = 0; i < 16; ++i) o[i >> 2] |= (uint32_t)tb[src[3 * i]] << (8 * (i & 3));
-      if (minus) {
-        const uint32_t t0 = o[0], t1 = o[1];
-        o[0] = __builtin_amdgcn_perm(0u, o[3], 0x00010203u);
-        o[1] = __builtin_amdgcn_perm(0u, o[2], 0x00010203u);
-        o[2] = __builtin_amdgcn_perm(0u, t1, 0x00010203u);
-        o[3] = __builtin_amdgcn_perm(0u, t0, 0x00010203u);
-      }
-      if (rem < 16) {  // stream end: the padding bytes are zero
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t drop = (uint32_t)min(max(4 * j + 4 - rem, 0), 4);  // bytes of word j
-          o[j] &= (uint32_t)(0xFFFFFFFFull >> (8 * drop));
-        }
-      }
-      *reinterpret_cast<uint4*>(a.out + g.out0 + 16 * (uint64_t)q) =
-          make_uint4(o[0], o[1], o[2], o[3]);
+    for (uint32_t q0 = 0; q0 < n_chunks; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      if (q0 + 64 <= n_minus) orf_chunks<1>(a, stage, s_tbl, seg, bm, pre, q, n_chunks);
+      else if (q0 >= n_minus) orf_chunks<0>(a, stage, s_tbl, seg, bm, pre, q, n_chunks);
+      else orf_chunks<2>(a, stage, s_tbl, seg, bm, pre, q, n_chunks);
     }
     if (!more) break;
     __builtin_amdgcn_wave_barrier();  // segment tables are rewritten
