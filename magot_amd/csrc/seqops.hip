@@ -309,33 +309,38 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
 #pragma unroll
     for (int k = 0; k < kPer; ++k) s_stage[wave][lane + 64 * k] = v[k];
   } else {
-    // the window's intervals (<= kOrf6RowCap, host-planned): {anchor, start}
-    uint64_t* const row = s_scratch[wave];
+    // the window's intervals (<= kOrf6RowCap, host-planned), rebased once to
+    // the window so that the per-vector math is 32-bit: {byte offset of the
+    // plane word holding window position 0 (mod 2^32: only positions inside
+    // the interval are read), 4 * nibble shift, window-relative start}
+    uint4* const row = reinterpret_cast<uint4*>(s_scratch[wave]);
     uint32_t* const cnt = reinterpret_cast<uint32_t*>(s_stage[wave]);  // 256 counters, then map
     const uint64_t e0 = a.tile_e0[tile];
-    uint64_t rs[2];
+    const int32_t wlen = (int32_t)(WE - W0);
+    int32_t rel[2];
     bool in[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const uint32_t jj = lane + 64 * h;
       const uint64_t j = min(e0 + (uint64_t)jj, a.n_rows);  // sentinel row n_rows
-      rs[h] = a.rows[2 * j + 1];
-      in[h] = jj <= kOrf6RowCap && rs[h] < WE;
-      if (jj <= kOrf6RowCap) {
-        row[2 * jj] = a.rows[2 * j];
-        row[2 * jj + 1] = rs[h];
-      }
+      const uint64_t A = a.rows[2 * j] + W0;                 // unified base of window position 0
+      const uint64_t st = a.rows[2 * j + 1];
+      const int64_t rs = (int64_t)(st - W0);
+      rel[h] = (int32_t)max(min(rs, (int64_t)(1 << 30)), -(int64_t)(1 << 30));
+      in[h] = jj <= kOrf6RowCap && st < WE;
+      if (jj <= kOrf6RowCap)
+        row[jj] = make_uint4((uint32_t)(A >> 3) << 2, 4u * (uint32_t)(A & 7u), (uint32_t)rel[h], 0u);
     }
     s_stage[wave][lane] = make_uint4(0u, 0u, 0u, 0u);
     const uint32_t m = (uint32_t)(__popcll(__ballot(in[0])) + __popcll(__ballot(in[1])));
     __builtin_amdgcn_wave_barrier();
     // first interval of every vector: count interval starts per vector
-    // (a start in (P_v - 16, P_v] counts at vector v), then prefix sums
+    // (a start in (16v - 16, 16v] counts at vector v), then prefix sums
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if (in[h]) {
-        const uint64_t v = rs[h] <= W0 ? 0 : (rs[h] - W0 + 15) >> 4;
-        if (v < (uint64_t)kOrfVecs) atomicAdd(&cnt[v], 1u);
+        const int32_t v = rel[h] <= 0 ? 0 : (rel[h] + 15) >> 4;
+        if (v < kOrfVecs) atomicAdd(&cnt[v], 1u);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -352,47 +357,69 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
       s_stage[wave][lane] = make_uint4(base + c0, base + c1, base + c2, base + c3);
     }
     __builtin_amdgcn_wave_barrier();
-    // e-bytes of vector t: its first interval's plane words for all four
-    // vectors in flight at once; the rest of a vector that crosses into
-    // later intervals afterwards
-    uint32_t iv[kPer], wv[kPer][3];
+    // Fast path: a vector spans at most two intervals, and the windows of
+    // both for all four vectors are in flight at once (one memory round
+    // trip).  A vector that reaches a third interval (intervals shorter than
+    // 16 bases) patches the rest afterwards.  Loads past the plane return 0.
+    const __amdgpu_buffer_rsrc_t plane = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(a.nib), (short)0,
+        (int)(uint32_t)min(a.nib_words * 4, (uint64_t)0xFFFFFFFFu), 0x00020000);
+    uint32_t iv[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) iv[k] = min(cnt[lane + 64 * k], m - 1);
+    uint32_t wa[kPer][3], wb[kPer][3];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-      const uint64_t P = W0 + 16 * (uint64_t)(lane + 64 * k);
-      const uint64_t u = row[2 * iv[k]] + P;  // chunk byte j <- unified base u + j
-      const uint32_t* w = a.nib + min(u >> 3, a.nib_words - 3);  // clamp: never off the plane
-      wv[k][0] = w[0];
-      wv[k][1] = w[1];
-      wv[k][2] = w[2];
+      const int32_t t16 = 16 * (lane + 64 * k);
+      const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];
+      const auto va = __builtin_amdgcn_raw_buffer_load_b96(plane, r0.x + (uint32_t)t16 / 2u, 0, 0);
+      wa[k][0] = va[0];
+      wa[k][1] = va[1];
+      wa[k][2] = va[2];
+      // branch-free: a vector inside one interval loads from past the
+      // plane's end, which the buffer range check answers with zeros and
+      // no memory request
+      const uint32_t ob =
+          (int32_t)r1.z < min(t16 + 16, wlen) ? r1.x + (uint32_t)t16 / 2u : 0xFFFFFFF0u;
+      const auto vb = __builtin_amdgcn_raw_buffer_load_b96(plane, ob, 0, 0);
+      wb[k][0] = vb[0];
+      wb[k][1] = vb[1];
+      wb[k][2] = vb[2];
     }
+    __builtin_amdgcn_sched_barrier(0);  // every window load is issued before the first is consumed
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t t = lane + 64 * k;
-      const uint64_t P = W0 + 16 * (uint64_t)t;
-      const uint64_t end = min(P + 16, WE);
-      uint32_t i = iv[k];
-      uint64_t u = row[2 * i] + P;
-      uint32_t sh = 4u * (uint32_t)(u & 7);
-      uint32_t x0 = funnel4(wv[k][1], wv[k][0], sh), x1 = funnel4(wv[k][2], wv[k][1], sh);
-      uint64_t pos = min(row[2 * i + 3], end);  // first interval ends here
-      while (pos < end) {  // later intervals of this vector
-        ++i;
-        u = row[2 * i] + P;
-        const uint32_t* w = a.nib + min(u >> 3, a.nib_words - 3);
-        sh = 4u * (uint32_t)(u & 7);
-        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-        const uint32_t j0 = (uint32_t)(pos - P);
-        const uint32_t n = (uint32_t)(min(row[2 * i + 3], end) - pos);
-        const uint64_t msk = (n >= 16 ? ~0ull : ((1ull << (4 * n)) - 1ull)) << (4 * j0);
-        x0 = (funnel4(w1, w0, sh) & (uint32_t)msk) | (x0 & ~(uint32_t)msk);
-        x1 = (funnel4(w2, w1, sh) & (uint32_t)(msk >> 32)) | (x1 & ~(uint32_t)(msk >> 32));
-        pos += n;
+      const int32_t t16 = 16 * (int32_t)t;
+      const int32_t et = min(t16 + 16, wlen);
+      const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];  // re-read: fewer live registers
+      const bool cross = (int32_t)r1.z < et;
+      // nibbles [j0, 16) come from the second interval (none: j0 = 16)
+      const uint32_t j0 = cross ? (uint32_t)((int32_t)r1.z - t16) : 16u;
+      const uint64_t mb = j0 >= 16 ? 0ull : ~0ull << (4 * j0);
+      const uint32_t x0 = funnel4(wa[k][1], wa[k][0], r0.y), x1 = funnel4(wa[k][2], wa[k][1], r0.y);
+      const uint32_t b0 = funnel4(wb[k][1], wb[k][0], r1.y), b1 = funnel4(wb[k][2], wb[k][1], r1.y);
+      uint32_t y0 = (b0 & (uint32_t)mb) | (x0 & ~(uint32_t)mb);
+      uint32_t y1 = (b1 & (uint32_t)(mb >> 32)) | (x1 & ~(uint32_t)(mb >> 32));
+      if (cross) {
+        uint32_t i = iv[k] + 2;  // rows up to iv + 2 start before WE or are staged
+        int32_t pos = (int32_t)row[i].z;
+        while (pos < et) {  // rare: later intervals inside this vector
+          const uint4 r = row[i];
+          const int32_t nxt = min((int32_t)row[i + 1].z, et);
+          const auto w = __builtin_amdgcn_raw_buffer_load_b96(plane, r.x + (uint32_t)t16 / 2u, 0, 0);
+          const uint32_t c0 = funnel4(w[1], w[0], r.y), c1 = funnel4(w[2], w[1], r.y);
+          const uint32_t j = (uint32_t)(pos - t16), n = (uint32_t)(nxt - pos);
+          const uint64_t msk = (n >= 16 ? ~0ull : ((1ull << (4 * n)) - 1ull)) << (4 * j);
+          y0 = (c0 & (uint32_t)msk) | (y0 & ~(uint32_t)msk);
+          y1 = (c1 & (uint32_t)(msk >> 32)) | (y1 & ~(uint32_t)(msk >> 32));
+          pos = nxt;
+          ++i;
+        }
       }
       uint32_t e[4];
-      nibbles_to_e(x0, e[0], e[1]);
-      nibbles_to_e(x1, e[2], e[3]);
+      nibbles_to_e(y0, e[0], e[1]);
+      nibbles_to_e(y1, e[2], e[3]);
       s_stage[wave][t] = make_uint4(e[0], e[1], e[2], e[3]);
     }
   }
