@@ -226,6 +226,9 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
                                            const uint32_t* bm, const uint32_t* pre, uint32_t q,
                                            uint32_t n_chunks) {
   if (q >= n_chunks) return;
+  // opaque per iteration: keeps the compiler from hoisting lane-invariant
+  // address terms of all three variants out of the chunk loop (and spilling)
+  __asm__ volatile("" : "+v"(q));
   const uint32_t wq = q >> 5;
   const uint32_t rank = pre[wq] + __popc(bm[wq] & (0xFFFFFFFFu >> (31 - (q & 31))));
   const OrfSeg g = seg[rank - 1];
@@ -235,9 +238,32 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
   // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed below)
   const uint8_t* const src = stage + (minus ? p - 45 : p);
   const uint8_t* const tb = kMode == 2 ? tbl + (minus ? 128 : 0) : tbl + (kMode == 1 ? 128 : 0);
-  uint32_t o[4] = {0u, 0u, 0u, 0u};
+  // Consecutive chunks of a segment sit 48 bytes (12 banks) apart, so lanes
+  // q, q+8, q+16, q+24 of a half-wave would hit one bank with every staged
+  // byte read.  Lane group j = (q >> 3) & 3 reads its residue quads in the
+  // rotated order j, j+1, .. (3 banks further per step), which makes the 32
+  // reads of a half-wave over one segment conflict-free; the quads are
+  // rotated back in registers.
+  const uint32_t rj = (q >> 3) & 3u;
+  // byte offsets of the quads in read order, one per byte: 12 * ((s + rj) & 3)
+  const uint32_t qo = __builtin_amdgcn_alignbit(0x24180C00u, 0x24180C00u, 8u * rj);
+  uint32_t r[4];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) o[i >> 2] |= (uint32_t)tb[src[3 * i]] << (8 * (i & 3));
+  for (int s = 0; s < 4; ++s) {
+    const uint8_t* const qs = src + ((qo >> (8 * s)) & 0xFFu);
+    r[s] = (uint32_t)tb[qs[0]] | ((uint32_t)tb[qs[3]] << 8) | ((uint32_t)tb[qs[6]] << 16) |
+           ((uint32_t)tb[qs[9]] << 24);
+  }
+  uint32_t o[4];  // o[d] = r[(d - rj) & 3]: rotate by 2, then by 1
+  {
+    const bool j2 = (q & 16u) != 0, j1 = (q & 8u) != 0;
+    const uint32_t t0 = j2 ? r[2] : r[0], t1 = j2 ? r[3] : r[1];
+    const uint32_t t2 = j2 ? r[0] : r[2], t3 = j2 ? r[1] : r[3];
+    o[0] = j1 ? t3 : t0;
+    o[1] = j1 ? t0 : t1;
+    o[2] = j1 ? t1 : t2;
+    o[3] = j1 ? t2 : t3;
+  }
   if (minus) {
     const uint32_t t0 = o[0], t1 = o[1];
     o[0] = __builtin_amdgcn_perm(0u, o[3], 0x00010203u);
