@@ -287,7 +287,11 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
 //                  as nucleotides (C5: extraction fused with translation).
 template <bool kGenome>
 __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
-  __shared__ uint8_t s_tbl[256];   // residue of cidx: [0,128) '+', [128,256) '-'
+  // residue of cidx: [0,128) '+', [128,256) '-'.  Every wave writes the
+  // whole (identical) table and then reads only what it wrote itself, so no
+  // workgroup barrier (and no wait for the table load) precedes staging, and
+  // the table's fixed address folds into the LDS immediates.
+  __shared__ uint32_t s_tblw[64];
   __shared__ uint8_t s_code[256];  // byte -> 2-bit code, or 0x40 when not ACGTacgt
   __shared__ uint4 s_stage[kOpsThreads / 64][kOrfVecs];
   // per wave: the staging window's interval rows, then (same bytes) the
@@ -295,15 +299,18 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   constexpr int kScratch = 2 * (kOrf6RowCap + 1);
   static_assert(kScratch * 8 >= kOrfSegs * 16 + 2 * kOrfRankWords * 4, "scratch too small");
   __shared__ uint64_t s_scratch[kOpsThreads / 64][kScratch];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  s_tbl[threadIdx.x] = a.tables[threadIdx.x];
-  {
+  // wave-uniform (scalar) tile index: the tile's bounds and offsets are
+  // scalar loads and their 64-bit arithmetic runs on the SALU
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (!kGenome) {
     const uint32_t c = code_of(threadIdx.x);
     s_code[threadIdx.x] = (uint8_t)(c < 4 ? c : 0x40u);
+    __syncthreads();
   }
-  __syncthreads();
   const uint64_t tile = (uint64_t)blockIdx.x * (kOpsThreads / 64) + wave;
   if (tile >= a.n_tiles) return;  // wave-uniform
+  s_tblw[lane] = reinterpret_cast<const uint32_t*>(a.tables)[lane];
+  const uint8_t* const s_tbl = reinterpret_cast<const uint8_t*>(s_tblw);
   const uint64_t T0 = a.tile_t0[tile], T1 = a.tile_t0[tile + 1];
   const uint64_t W0 = (T0 >= 48 ? T0 - 48 : 0) & ~15ull;
   const uint64_t WE = min(T1 + 50, a.total);
@@ -317,13 +324,13 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   const bool my_plus = lane >= kOrfSegs / 2;
   const uint32_t my_s = 2u * my_f + (my_plus ? 1u : 0u);
   // the first record batch's offsets, in flight with the staging loads
+  // (unconditional clamped loads: a branch here would wait for them before
+  // the staging loads are issued)
   uint64_t rb = a.tile_r0[tile];
+  const uint64_t rr0 = min(rb + my_rec, a.n_rec - 1);
+  const uint64_t nb_first = a.noff[rr0], ne_first = a.noff[rr0 + 1];
   uint64_t nb = 0, L = 0;
-  bool rec = lane < kOrfSegs && rb + my_rec < a.n_rec;
-  if (rec) {
-    nb = a.noff[rb + my_rec];
-    L = a.noff[rb + my_rec + 1] - nb;
-  }
+  bool rec = false;
   if (!kGenome) {
     // raw bytes: all loads in flight at once, to LDS when they land
     uint4 v[kPer];
@@ -345,12 +352,17 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     const int32_t wlen = (int32_t)(WE - W0);
     int32_t rel[2];
     bool in[2];
+    ulonglong2 rw[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // sentinel row n_rows
+      const uint64_t j = min(e0 + (uint64_t)(lane + 64 * h), a.n_rows);
+      rw[h] = *reinterpret_cast<const ulonglong2*>(a.rows + 2 * j);
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const uint32_t jj = lane + 64 * h;
-      const uint64_t j = min(e0 + (uint64_t)jj, a.n_rows);  // sentinel row n_rows
-      const uint64_t A = a.rows[2 * j] + W0;                 // unified base of window position 0
-      const uint64_t st = a.rows[2 * j + 1];
+      const uint64_t A = rw[h].x + W0;  // unified base of window position 0
+      const uint64_t st = rw[h].y;
       const int64_t rs = (int64_t)(st - W0);
       rel[h] = (int32_t)max(min(rs, (int64_t)(1 << 30)), -(int64_t)(1 << 30));
       in[h] = jj <= kOrf6RowCap && st < WE;
@@ -457,10 +469,13 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   for (;; rb += kOrfBatch) {
     // ---- the batch's segments: one (record, stream) per lane
     const uint64_t r = rb + my_rec;
+    rec = lane < kOrfSegs && r < a.n_rec;
     if (staged) {
-      rec = lane < kOrfSegs && r < a.n_rec;
       nb = rec ? a.noff[r] : 0;
       L = rec ? a.noff[r + 1] - nb : 0;
+    } else {
+      nb = rec ? nb_first : 0;
+      L = rec ? ne_first - nb_first : 0;
     }
     const uint64_t nres = rec && nb < T1 ? orf_count(L, my_f) : 0;
     uint64_t lo = 0, hi = 0;
