@@ -234,7 +234,9 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
   const OrfSeg g = seg[rank - 1];
   const bool minus = kMode == 1 ? true : kMode == 0 ? false : g.rem0 < 0;
   const int32_t rem = (minus ? -g.rem0 : g.rem0) - 16 * (int32_t)q;
-  const int32_t p = g.p0 + (minus ? -48 : 48) * (int32_t)q;
+  int32_t m48 = (int32_t)__umul24(q, 48u);  // full-rate 24-bit multiply (kept
+  __asm__("" : "+v"(m48));                   // from folding into a -48 v_mul_lo)
+  const int32_t p = minus ? g.p0 - m48 : g.p0 + m48;
   // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed below)
   const uint8_t* const src = stage + (minus ? p - 45 : p);
   const uint8_t* const tb = kMode == 2 ? tbl + (minus ? 128 : 0) : tbl + (kMode == 1 ? 128 : 0);
@@ -251,8 +253,10 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const uint8_t* const qs = src + ((qo >> (8 * s)) & 0xFFu);
-    r[s] = (uint32_t)tb[qs[0]] | ((uint32_t)tb[qs[3]] << 8) | ((uint32_t)tb[qs[6]] << 16) |
-           ((uint32_t)tb[qs[9]] << 24);
+    // three ops per quad: two byte pairs, then one perm
+    const uint32_t lo = (uint32_t)tb[qs[0]] | ((uint32_t)tb[qs[3]] << 8);
+    const uint32_t hi = (uint32_t)tb[qs[6]] | ((uint32_t)tb[qs[9]] << 8);
+    r[s] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
   }
   uint32_t o[4];  // o[d] = r[(d - rj) & 3]: rotate by 2, then by 1
   {
