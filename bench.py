@@ -91,7 +91,10 @@ def allreduce_sum(dist, x):
 # genome.py:603-822), single core, on a bounded sample of the same workload.
 # ---------------------------------------------------------------------------
 
-def cpu_baseline(w, budget_bases):
+def cpu_baseline(w, budget_bases, orfs=False):
+    """orfs=False: get_fasta nucleotide + protein per record (C2/C3).
+    orfs=True (C5): get_fasta nucleotide, then Sequence.get_orfs on it
+    (genome.py:824-851: the six translations, split at stops)."""
     from oracle import magot_oracle as mo
     step = max(1, int(w.cds_bases // max(budget_bases, 1)))
     tx_ids = np.arange(0, w.n_tx, step)
@@ -118,16 +121,20 @@ def cpu_baseline(w, budget_bases):
         aset.mRNA[rna.ID] = rna
         recs.append(rna)
     t0 = time.perf_counter()
-    for r in recs:
-        mo.get_fasta(r, aset, 'nucleotide')
+    nucs = [mo.get_fasta(r, aset, 'nucleotide') for r in recs]
     t1 = time.perf_counter()
-    for r in recs:
-        mo.get_fasta(r, aset, 'protein')
+    if orfs:
+        for text in nucs:
+            mo.get_orfs(text.split('\n', 1)[1])
+    else:
+        for r in recs:
+            mo.get_fasta(r, aset, 'protein')
     t2 = time.perf_counter()
     rate = bases / (t2 - t0)
+    second = 'get_orfs (six frames)' if orfs else 'protein'
     cal = None
     cal_path = os.path.join(ROOT, 'profiles', 'cpu_calibration.json')
-    if os.path.exists(cal_path):
+    if os.path.exists(cal_path) and not orfs:  # calibrated on nucleotide + protein only
         with open(cal_path) as fh:
             ratio = json.load(fh)['port_over_reference_mean']
         # the reference's own loop (AnnotationSet.__getitem__ evals, genome.py:536-544)
@@ -136,9 +143,9 @@ def cpu_baseline(w, budget_bases):
                'source': 'profiles/cpu_calibration.json'}
     return {'value': rate, 'unit': 'bases/s', 'cores': 1, 'kind': 'port', 'calibration': cal,
             'sample': '%d of %d transcripts (every %d-th), %d CDS bases; get_fasta nucleotide '
-                      '%.2fs + protein %.2fs; pure-Python restatement of the reference loop '
+                      '%.2fs + %s %.2fs; pure-Python restatement of the reference loop '
                       '(oracle/magot_oracle.py)' % (len(recs), w.n_tx, step, bases, t1 - t0,
-                                                   t2 - t1)}
+                                                   second, t2 - t1)}
 
 
 def strong_main(args, dist, rank, local, world):
@@ -314,6 +321,14 @@ def orf6_main(args, dist, rank, local, world):
     # algorithmic bytes: 2-bit genome reads + six translations + descriptors
     alg = -(-B // 4) + R + 16 * int(plan.n_exons) + 32 * int(plan.n_tx)
     achieved = alg / (k_o6 * 1e-3) / 1e9
+    traffic = None
+    pmc5 = os.path.join(ROOT, 'profiles', 'pmc_C5.json')
+    if os.path.exists(pmc5):
+        with open(pmc5) as fh:
+            traffic = json.load(fh)['hbm_bytes_per_launch']
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(w, args.cpu_sample_bases / 10, orfs=True)
     if rank == 0:
         rec = {
             'metric': 'CDS bases extracted+translated/sec', 'value': total_bases * args.steps /
@@ -326,12 +341,12 @@ def orf6_main(args, dist, rank, local, world):
                        'cds_bases_per_rank': B, 'six_frame_residues_per_rank': R,
                        'parallelism': 'contig-sharded x%d (weak)' % world},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': None,
+                         'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'kernel': 'orf6_kernel (gather fused with six-frame translation)',
                          'kernel_ms': k_o6,
                          'extract_kernel_ms_nucleotide_only': k_ex,
                          'algorithmic_bytes_per_step': alg},
-            'cpu_baseline': None, 'parity': parity, 'phases_s': {'generate': t_gen},
+            'cpu_baseline': cpu, 'parity': parity, 'phases_s': {'generate': t_gen},
         }
         print(json.dumps(rec), flush=True)
     o6.close()

@@ -3,20 +3,21 @@
 Follows /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
 WRITE_SIZE come from separate passes; FETCH_SIZE (KiB, = TCC_EA0_RDREQ x 64 B)
 reports half the bytes of 128-B line fills on gfx950, so it is doubled;
-WRITE_SIZE is taken as is.   usage: pmc_traffic.py SUMMARY.json OUT.json [config]
+WRITE_SIZE is taken as is.   usage: pmc_traffic.py SUMMARY.json OUT.json [config] [kernel]
 """
 import json
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
 cfg = sys.argv[3] if len(sys.argv) > 3 else 'C3'
+kern = sys.argv[4] if len(sys.argv) > 4 else 'extract_kernel'
 pmc = json.load(open(src))
 flat = {}
 for grp in pmc.values():
     flat.update(grp)
 fetch = flat['FETCH_SIZE'] * 1024.0
 write = flat['WRITE_SIZE'] * 1024.0
-rec = {'config': cfg, 'kernel': 'extract_kernel', 'source': src,
+rec = {'config': cfg, 'kernel': kern, 'source': src,
        'fetch_size_bytes_raw': fetch, 'write_size_bytes': write,
        'hbm_read_bytes_per_launch': 2.0 * fetch,
        'hbm_bytes_per_launch': 2.0 * fetch + write,
