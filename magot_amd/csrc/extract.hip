@@ -15,8 +15,8 @@
 //     tiles of <= 3024 bytes (189 chunks of 16 bytes; shorter where a tile
 //     would touch more than kExonCap intervals or kTxCap records).  A tile
 //     belongs to ONE wavefront: 64 lanes x 3 chunk slots (189 output chunks +
-//     a halo chunk for codons that run past the tile end), so the only
-//     workgroup barrier is the one publishing the codon table.
+//     a halo chunk for codons that run past the tile end), so there is no
+//     workgroup barrier (every wave writes its own copy of the codon table).
 //   * Staging: the tile's intervals go to wave-private LDS as {64-bit unified
 //     anchor, tile-relative end, flags}; chunk -> interval and residue chunk
 //     -> record maps come from an LDS histogram + one packed DPP wave scan.
@@ -368,7 +368,7 @@ __device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, uint32
 
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   __shared__ WaveLds s_wave[kWaves];
-  __shared__ uint8_t s_lut[64];
+  __shared__ __attribute__((aligned(16))) uint8_t s_lut[64];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -379,16 +379,21 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   const bool want_nuc = (a.outputs & MAGOT_OUT_NUC) != 0;
   const bool want_pep = (a.outputs & MAGOT_OUT_PEP) != 0;
 
-  if (threadIdx.x < 64)
-    s_lut[threadIdx.x] = (a.lut[threadIdx.x >> 2] >> (8 * (threadIdx.x & 3))) & 0xFFu;
+  const uint32_t t = blockIdx.x * kWaves + wave;
+  if (t >= a.n_tiles) return;
+  // Every wave writes the whole (identical) codon table from scalar kernel
+  // arguments and then reads only what it wrote itself: no workgroup
+  // barrier and no memory round trip before the tile's own loads.
+  {
+    uint32_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v = lane == i ? a.lut[i] : v;
+    if (lane < 16) reinterpret_cast<uint32_t*>(s_lut)[lane] = v;
+  }
   if (lane < kGuard) {
     L.codes_g[lane] = 0;
     L.valid_g[lane] = 0;
   }
-  __syncthreads();  // the only block-level barrier: s_lut
-
-  const uint32_t t = blockIdx.x * kWaves + wave;
-  if (t >= a.n_tiles) return;
   const TileDesc d = load_desc(a, t);
   const TileGeom g = geom(a, d);
   stage(L, codes, valid32, d, g, load_rows(a, d, lane), a.span, lane);
