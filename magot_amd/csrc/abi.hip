@@ -1025,7 +1025,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
     const uint64_t gw = ex_g[i], o0 = ex_out[i], len = ex_out[i + 1] - o0;
     const uint64_t gs = gw & ~(kRcBit | kExcBit);
     rows[2 * i] = (gw & kRcBit) ? 2 * span - gs - len - o0 : gs - o0;
-    rows[2 * i + 1] = o0;
+    rows[2 * i + 1] = o0 | ((gw & kExcBit) ? kOrf6ExcRow : 0ull);  // the exact path's flag
     starts[i] = o0;
   }
   rows[2 * ne] = 0;
@@ -1047,11 +1047,22 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   const uint64_t o_r0 = cv.take<uint32_t>(n_tiles);
   const uint64_t o_e0 = cv.take<uint32_t>(n_tiles);
   const uint64_t o_lut = cv.take<uint8_t>(256);
+  const uint64_t nib_words = p->args.span / 4;  // forward + reverse planes, 8 bases per word
+  const uint64_t code2_words = nib_words / 2;
+  const uint64_t o_code2 = cv.take<uint32_t>(code2_words + 4);
+  const uint64_t exc1_words = nib_words / 4;
+  const uint64_t o_exc1 = cv.take<uint32_t>(exc1_words + 4);
   MAGOT_HIP_TRY(hipMalloc(&o->arena, cv.used));
   char* base = static_cast<char*>(o->arena);
   auto up = [&](uint64_t off, const void* src, uint64_t bytes) {
     return bytes ? hipMemcpy(base + off, src, bytes, hipMemcpyHostToDevice) : hipSuccess;
   };
+  uint32_t* code2 = reinterpret_cast<uint32_t*>(base + o_code2);
+  uint32_t* exc1 = reinterpret_cast<uint32_t*>(base + o_exc1);
+  launch_code2(p->args.nib, nib_words, code2, ctx->stream);
+  launch_exc1(p->args.nib, nib_words, exc1, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   MAGOT_HIP_TRY(up(o_off, p->nuc_off.data(), (o->n_rec + 1) * 8));
   MAGOT_HIP_TRY(up(o_soff, o->host_soff.data(), (6 * o->n_rec + 1) * 8));
   MAGOT_HIP_TRY(up(o_rows, rows.data(), rows.size() * 8));
@@ -1062,7 +1073,11 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   o->out = reinterpret_cast<uint8_t*>(base + o_out);
   Orf6Args& a = o->args;
   a.nib = p->args.nib;
-  a.nib_words = p->args.span / 4;  // forward + reverse planes, 8 bases per word
+  a.nib_words = nib_words;
+  a.code2 = code2;
+  a.code2_words = code2_words;
+  a.exc1 = exc1;
+  a.exc1_words = exc1_words;
   a.rows = reinterpret_cast<const uint64_t*>(base + o_rows);
   a.n_rows = ne;
   a.noff = reinterpret_cast<const uint64_t*>(base + o_off);

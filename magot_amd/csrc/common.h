@@ -145,10 +145,15 @@ void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t
 // Tiles (orf6_plan_tiles): t0 = n_tiles+1 starts, r0 = record holding each
 // start, e0 = interval holding each staged window's first base.
 constexpr uint32_t kOrf6RowCap = 123;  // intervals per staged window
+constexpr uint64_t kOrf6ExcRow = 1ull << 63;  // row start flag: the interval touches an exception run
 struct Orf6Args {
   const uint8_t* nuc;
   const uint32_t* nib;
-  uint64_t nib_words;  // both planes
+  uint64_t nib_words;      // both planes
+  const uint32_t* code2;   // 2-bit codes of the same unified bases, 16 per word
+  uint64_t code2_words;    // = nib_words / 2
+  const uint32_t* exc1;    // exception bits of the same unified bases, 32 per word
+  uint64_t exc1_words;     // = nib_words / 4
   const uint64_t* rows;
   uint64_t n_rows;
   const uint64_t* noff;
@@ -170,6 +175,12 @@ void orf6_tables(const uint8_t lut64[64], uint8_t out[256]);
 void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_start,
                      uint64_t n_rows, Orf6Tiles* out);
 void launch_orf6(const Orf6Args& a, bool genome, hipStream_t s);
+// The 2-bit code plane of a nibble plane (nib_words words, 8 bases each):
+// word w holds the codes of unified bases 16w .. 16w+15 (base k at bits 2k).
+void launch_code2(const uint32_t* nib, uint64_t nib_words, uint32_t* code2, hipStream_t s);
+// The exception-bit plane: word w holds bit 3 of the nibbles of unified bases
+// 32w .. 32w+31 (base k at bit k).
+void launch_exc1(const uint32_t* nib, uint64_t nib_words, uint32_t* exc1, hipStream_t s);
 void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const int32_t* frames,
                       const uint8_t* strands, const uint64_t* pep_off, uint64_t total_pep,
                       const uint32_t* lut16, uint8_t* out, hipStream_t s);

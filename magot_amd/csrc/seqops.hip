@@ -366,12 +366,17 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     for (int h = 0; h < 2; ++h) {
       const uint32_t jj = lane + 64 * h;
       const uint64_t A = rw[h].x + W0;  // unified base of window position 0
-      const uint64_t st = rw[h].y;
+      const uint64_t st = rw[h].y & ~kOrf6ExcRow;
       const int64_t rs = (int64_t)(st - W0);
       rel[h] = (int32_t)max(min(rs, (int64_t)(1 << 30)), -(int64_t)(1 << 30));
       in[h] = jj <= kOrf6RowCap && st < WE;
+      // {code-plane byte offset of the word holding window position 0,
+      //  A & 31 | exception flag << 5, window-relative start,
+      //  exception-plane byte offset of the word holding window position 0}
       if (jj <= kOrf6RowCap)
-        row[jj] = make_uint4((uint32_t)(A >> 3) << 2, 4u * (uint32_t)(A & 7u), (uint32_t)rel[h], 0u);
+        row[jj] = make_uint4((uint32_t)(A >> 4) << 2,
+                             (uint32_t)(A & 31u) | ((rw[h].y & kOrf6ExcRow) ? 32u : 0u),
+                             (uint32_t)rel[h], (uint32_t)(A >> 5) << 2);
     }
     s_stage[wave][lane] = make_uint4(0u, 0u, 0u, 0u);
     const uint32_t m = (uint32_t)(__popcll(__ballot(in[0])) + __popcll(__ballot(in[1])));
@@ -399,77 +404,157 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
       s_stage[wave][lane] = make_uint4(base + c0, base + c1, base + c2, base + c3);
     }
     __builtin_amdgcn_wave_barrier();
-    // Fast path: a vector spans at most two intervals, and the windows of
-    // both for all four vectors are in flight at once (one memory round
-    // trip).  A vector that reaches a third interval (intervals shorter than
-    // 16 bases) patches the rest afterwards.  Loads past the plane return 0.
-    const __amdgpu_buffer_rsrc_t plane = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(a.nib), (short)0,
-        (int)(uint32_t)min(a.nib_words * 4, (uint64_t)0xFFFFFFFFu), 0x00020000);
+    // Codon indices straight from the 2-bit code plane: translation ignores
+    // case, so a vector needs only the codes of its 16 positions and of the
+    // next two, plus, where an interval touches an exception run (flagged by
+    // the host), the exception bits of those positions (1 bit per base).
+    // Fast path: the 18 positions span at most two intervals, and every
+    // window of all four vectors is in flight at once (one memory round
+    // trip).  A window that is not needed (no second interval, interval not
+    // flagged) is read from past the plane's end, which the buffer range
+    // check answers with zeros and no memory request.
+    const __amdgpu_buffer_rsrc_t plane2 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(a.code2), (short)0,
+        (int)(uint32_t)min(a.code2_words * 4, (uint64_t)0xFFFFFFFFu), 0x00020000);
+    const __amdgpu_buffer_rsrc_t plane1 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(a.exc1), (short)0,
+        (int)(uint32_t)min(a.exc1_words * 4, (uint64_t)0xFFFFFFFFu), 0x00020000);
     uint32_t iv[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) iv[k] = min(cnt[lane + 64 * k], m - 1);
-    uint32_t wa[kPer][3], wb[kPer][3];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int32_t t16 = 16 * (lane + 64 * k);
-      const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];
-      const auto va = __builtin_amdgcn_raw_buffer_load_b96(plane, r0.x + (uint32_t)t16 / 2u, 0, 0);
-      wa[k][0] = va[0];
-      wa[k][1] = va[1];
-      wa[k][2] = va[2];
-      // branch-free: a vector inside one interval loads from past the
-      // plane's end, which the buffer range check answers with zeros and
-      // no memory request
-      const uint32_t ob =
-          (int32_t)r1.z < min(t16 + 16, wlen) ? r1.x + (uint32_t)t16 / 2u : 0xFFFFFFF0u;
-      const auto vb = __builtin_amdgcn_raw_buffer_load_b96(plane, ob, 0, 0);
-      wb[k][0] = vb[0];
-      wb[k][1] = vb[1];
-      wb[k][2] = vb[2];
-    }
-    __builtin_amdgcn_sched_barrier(0);  // every window load is issued before the first is consumed
+    uint32_t wa[kPer][3], wb[kPer][3], xa[kPer][2], xb[kPer][2];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t t = lane + 64 * k;
       const int32_t t16 = 16 * (int32_t)t;
-      const int32_t et = min(t16 + 16, wlen);
+      const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];
+      const bool cross = (int32_t)r1.z < min(t16 + 18, wlen);
+      const auto va = __builtin_amdgcn_raw_buffer_load_b96(plane2, r0.x + 4u * t, 0, 0);
+      const auto vb =
+          __builtin_amdgcn_raw_buffer_load_b96(plane2, cross ? r1.x + 4u * t : 0xFFFFFFF0u, 0, 0);
+      const uint32_t ea = r0.w + 4u * (((r0.y & 31u) + 16u * t) >> 5);
+      const uint32_t eb = r1.w + 4u * (((r1.y & 31u) + 16u * t) >> 5);
+      const auto ua = __builtin_amdgcn_raw_buffer_load_b64(plane1, (r0.y & 32u) ? ea : 0xFFFFFFF0u, 0, 0);
+      const auto ub = __builtin_amdgcn_raw_buffer_load_b64(
+          plane1, (cross && (r1.y & 32u)) ? eb : 0xFFFFFFF0u, 0, 0);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        wa[k][d] = va[d];
+        wb[k][d] = vb[d];
+      }
+      xa[k][0] = ua[0];
+      xa[k][1] = ua[1];
+      xb[k][0] = ub[0];
+      xb[k][1] = ub[1];
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every window load is issued before the first is consumed
+    uint32_t exact = 0;  // bit k: vector k takes the exact path below
+    bool any_exc = false;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t t = lane + 64 * k;
+      const int32_t t16 = 16 * (int32_t)t;
+      const int32_t et = min(t16 + 18, wlen);
       const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];  // re-read: fewer live registers
       const bool cross = (int32_t)r1.z < et;
-      // nibbles [j0, 16) come from the second interval (none: j0 = 16)
-      const uint32_t j0 = cross ? (uint32_t)((int32_t)r1.z - t16) : 16u;
-      const uint64_t mb = j0 >= 16 ? 0ull : ~0ull << (4 * j0);
-      const uint32_t x0 = funnel4(wa[k][1], wa[k][0], r0.y), x1 = funnel4(wa[k][2], wa[k][1], r0.y);
-      const uint32_t b0 = funnel4(wb[k][1], wb[k][0], r1.y), b1 = funnel4(wb[k][2], wb[k][1], r1.y);
-      uint32_t y0 = (b0 & (uint32_t)mb) | (x0 & ~(uint32_t)mb);
-      uint32_t y1 = (b1 & (uint32_t)(mb >> 32)) | (x1 & ~(uint32_t)(mb >> 32));
-      if (cross) {
-        uint32_t i = iv[k] + 2;  // rows up to iv + 2 start before WE or are staged
-        int32_t pos = (int32_t)row[i].z;
-        while (pos < et) {  // rare: later intervals inside this vector
+      // positions [j0, 18) come from the second interval (none: j0 = 32)
+      const uint32_t j0 = cross ? (uint32_t)((int32_t)r1.z - t16) : 32u;
+      const uint64_t mb = j0 >= 32 ? 0ull : ~0ull << (2 * j0);
+      const uint32_t sa = 2u * (r0.y & 15u), sb = 2u * (r1.y & 15u);
+      const uint32_t x0 = funnel4(wa[k][1], wa[k][0], sa), x1 = funnel4(wa[k][2], wa[k][1], sa);
+      const uint32_t b0 = funnel4(wb[k][1], wb[k][0], sb), b1 = funnel4(wb[k][2], wb[k][1], sb);
+      const uint32_t y0 = (b0 & (uint32_t)mb) | (x0 & ~(uint32_t)mb);
+      const uint32_t y1 = (b1 & (uint32_t)(mb >> 32)) | (x1 & ~(uint32_t)(mb >> 32));
+      if (cross && (int32_t)row[iv[k] + 2].z < et) exact |= 1u << k;
+      // exception bits of positions 0..17: bit j set = base j not ACGTacgt
+      const uint32_t ma = j0 >= 32 ? 0u : ~0u << j0;
+      const uint32_t va = funnel4(xa[k][1], xa[k][0], ((r0.y & 31u) + 16u * t) & 31u);
+      const uint32_t vb = funnel4(xb[k][1], xb[k][0], ((r1.y & 31u) + 16u * t) & 31u);
+      const uint32_t ex = (vb & ma) | (va & ~ma);
+      any_exc |= ex != 0;
+      xa[k][0] = ex;  // reused below
+      // cidx byte i = codes of positions i, i+1, i+2 = bits [2i, 2i+6)
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t z = j == 0 ? y0 : funnel4(y1, y0, 8u * j);
+        // four bit-field extracts and three shift-ors
+        const uint32_t lo = __builtin_amdgcn_ubfe(z, 0, 6) | (__builtin_amdgcn_ubfe(z, 2, 6) << 8);
+        const uint32_t hi = __builtin_amdgcn_ubfe(z, 4, 6) | (__builtin_amdgcn_ubfe(z, 6, 6) << 8);
+        o[j] = lo | (hi << 16);
+      }
+      s_stage[wave][t] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    if (__builtin_amdgcn_readfirstlane(__ballot(any_exc) != 0)) {
+      // codon i is invalid ('X') when any of positions i, i+1, i+2 is an
+      // exception: set bit 6 of its index
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const uint32_t ex = xa[k][0];
+        if (ex) {
+          const uint32_t t = lane + 64 * k;
+          const uint32_t inv = ex | (ex >> 1) | (ex >> 2);
+          uint4 c = s_stage[wave][t];
+          uint32_t* const cw = reinterpret_cast<uint32_t*>(&c);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            cw[j] |= ((__umul24((inv >> (4 * j)) & 15u, 0x204081u) & 0x01010101u) << 6);
+          s_stage[wave][t] = c;
+        }
+      }
+    }
+    if (__builtin_amdgcn_readfirstlane(__ballot(exact != 0) != 0)) {
+      // Exact path (rare): vectors over an exception run or over three or
+      // more intervals rebuild their 18 positions from the nibble plane,
+      // interval by interval, as e-bytes (code | exception << 6).
+      const __amdgpu_buffer_rsrc_t plane = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint32_t*>(a.nib), (short)0,
+          (int)(uint32_t)min(a.nib_words * 4, (uint64_t)0xFFFFFFFFu), 0x00020000);
+#pragma unroll 1
+      for (int k = 0; k < kPer; ++k) {
+        if (!((exact >> k) & 1u)) continue;
+        const uint32_t t = lane + 64 * k;
+        const int32_t t16 = 16 * (int32_t)t;
+        const int32_t et = min(t16 + 18, wlen);
+        uint32_t x[3] = {0u, 0u, 0u};  // nibbles of positions 0..17 (x[2]: 16, 17)
+        uint32_t i = iv[k];
+        int32_t pos = t16;
+        while (pos < et) {
           const uint4 r = row[i];
           const int32_t nxt = min((int32_t)row[i + 1].z, et);
-          const auto w = __builtin_amdgcn_raw_buffer_load_b96(plane, r.x + (uint32_t)t16 / 2u, 0, 0);
-          const uint32_t c0 = funnel4(w[1], w[0], r.y), c1 = funnel4(w[2], w[1], r.y);
-          const uint32_t j = (uint32_t)(pos - t16), n = (uint32_t)(nxt - pos);
-          const uint64_t msk = (n >= 16 ? ~0ull : ((1ull << (4 * n)) - 1ull)) << (4 * j);
-          y0 = (c0 & (uint32_t)msk) | (y0 & ~(uint32_t)msk);
-          y1 = (c1 & (uint32_t)(msk >> 32)) | (y1 & ~(uint32_t)(msk >> 32));
+          // nibble-plane byte offset of the word holding window position 0
+          const uint32_t nboff = 2u * r.x + 4u * ((r.y >> 3) & 1u);
+          const uint32_t sh = 4u * (r.y & 7u);
+          const auto w = __builtin_amdgcn_raw_buffer_load_b128(plane, nboff + 8u * t, 0, 0);
+          const uint32_t c[3] = {funnel4(w[1], w[0], sh), funnel4(w[2], w[1], sh),
+                                 funnel4(w[3], w[2], sh)};
+          const int32_t j = pos - t16, n = nxt - pos;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const int32_t lo = max(j - 8 * q, 0), hi = min(j + n - 8 * q, 8);
+            if (lo < hi) {
+              const uint32_t mh = hi >= 8 ? ~0u : (1u << (4 * hi)) - 1u;
+              const uint32_t ml = (1u << (4 * lo)) - 1u;
+              const uint32_t msk = mh & ~ml;
+              x[q] = (c[q] & msk) | (x[q] & ~msk);
+            }
+          }
           pos = nxt;
           ++i;
         }
+        uint32_t e[6];
+        nibbles_to_e(x[0], e[0], e[1]);
+        nibbles_to_e(x[1], e[2], e[3]);
+        nibbles_to_e(x[2], e[4], e[5]);
+        s_stage[wave][t] = codon_indices(e);
       }
-      uint32_t e[4];
-      nibbles_to_e(y0, e[0], e[1]);
-      nibbles_to_e(y1, e[2], e[3]);
-      s_stage[wave][t] = make_uint4(e[0], e[1], e[2], e[3]);
     }
   }
   const uint8_t* const stage = reinterpret_cast<const uint8_t*>(s_stage[wave]);
   OrfSeg* const seg = reinterpret_cast<OrfSeg*>(s_scratch[wave]);
   uint32_t* const bm = reinterpret_cast<uint32_t*>(s_scratch[wave] + 2 * kOrfSegs);
   uint32_t* const pre = bm + kOrfRankWords;
-  bool staged = false;
+  bool staged = kGenome;  // the gather stages codon indices directly
   for (;; rb += kOrfBatch) {
     // ---- the batch's segments: one (record, stream) per lane
     const uint64_t r = rb + my_rec;
@@ -582,7 +667,57 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   }
 }
 
+// 2-bit code plane: word w = codes of unified bases 16w .. 16w+15 (nibble
+// words 2w, 2w+1), base k at bits 2k.  Exception bases (code bits 0 in the
+// nibble plane) become 'A'; the orf6 rows flag their intervals.
+__global__ __launch_bounds__(256) void code2_kernel(const uint32_t* __restrict__ nib,
+                                                    uint64_t n_words, uint32_t* __restrict__ code2) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_words) return;
+  const uint2 x = reinterpret_cast<const uint2*>(nib)[w];
+  // per byte: code(2k) | code(2k+1) << 2 in the low nibble, then four codes
+  // in bytes 0 and 2
+  const uint32_t y0 = (x.x & 0x03030303u) | ((x.x >> 2) & 0x0C0C0C0Cu);
+  const uint32_t y1 = (x.y & 0x03030303u) | ((x.y >> 2) & 0x0C0C0C0Cu);
+  const uint32_t z0 = (y0 & 0x0F0F0F0Fu) | ((y0 >> 4) & 0xF0F0F0F0u);
+  const uint32_t z1 = (y1 & 0x0F0F0F0Fu) | ((y1 >> 4) & 0xF0F0F0F0u);
+  code2[w] = __builtin_amdgcn_perm(z1, z0, 0x06040200u);
+}
+
+// Exception-bit plane: word w = bit 3 of the nibbles of unified bases 32w ..
+// 32w+31 (nibble words 4w .. 4w+3), base k at bit k.
+__global__ __launch_bounds__(256) void exc1_kernel(const uint32_t* __restrict__ nib,
+                                                   uint64_t n_words, uint32_t* __restrict__ exc1) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (w >= n_words) return;
+  const uint4 x = reinterpret_cast<const uint4*>(nib)[w];
+  const uint32_t v[4] = {x.x, x.y, x.z, x.w};
+  uint32_t out = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    uint32_t y = (v[q] >> 3) & 0x11111111u;  // bits 0, 4, .., 28
+    y = (y | (y >> 3)) & 0x03030303u;        // two per byte
+    y = (y | (y >> 6)) & 0x000F000Fu;        // four per half
+    y = (y | (y >> 12)) & 0xFFu;             // eight
+    out |= y << (8 * q);
+  }
+  exc1[w] = out;
+}
+
 }  // namespace
+
+void launch_exc1(const uint32_t* nib, uint64_t nib_words, uint32_t* exc1, hipStream_t s) {
+  const uint64_t n = nib_words / 4;
+  if (n == 0) return;
+  hipLaunchKernelGGL(exc1_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, nib, n, exc1);
+}
+
+void launch_code2(const uint32_t* nib, uint64_t nib_words, uint32_t* code2, hipStream_t s) {
+  const uint64_t n = nib_words / 2;
+  if (n == 0) return;
+  hipLaunchKernelGGL(code2_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, nib, n,
+                     code2);
+}
 
 void orf6_tables(const uint8_t lut64[64], uint8_t out[256]) {
   // '+': cidx = c0 | c1 << 2 | c2 << 4 indexes the library directly;
