@@ -13,11 +13,11 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py --steps 20 --warmup 3"
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 if has tests; then
-  timeout -k 10 900 python -m pytest tests -m "gpu and not slow" -q > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m "gpu and not slow" -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
   tail -1 $OUT/pytest_gpu.log
 fi
 if has slow; then
-  timeout -k 10 900 python -m pytest tests -m "gpu and slow" -q > $OUT/pytest_gpu_slow.log 2>&1 || { tail -40 $OUT/pytest_gpu_slow.log; exit 1; }
+  timeout -k 10 900 python -u -m pytest tests -m "gpu and slow" -q --timeout 600 --timeout-method thread > $OUT/pytest_gpu_slow.log 2>&1 || { tail -40 $OUT/pytest_gpu_slow.log; exit 1; }
   tail -1 $OUT/pytest_gpu_slow.log
 fi
 if has bench; then
