@@ -456,6 +456,55 @@ def test_orf6_fused_gather_tiny_intervals_vs_oracle():
     dev.close()
 
 
+def test_orf6_fused_code_plane_boundaries_vs_oracle():
+    """The fused gather's 2-bit fast path at its edges: intervals of 14-20
+    bases put the second (and third) interval exactly at the 16th-18th
+    position of a vector, on both strands, over a genome dense in IUPAC
+    bytes and N runs (the exception plane and the per-interval flags), plus
+    long intervals that cross many vectors."""
+    rng = np.random.default_rng(61)
+    w = synth.make('small', seed=61, genome_bases=400_000, n_tx=10, iupac_rate=2e-2)
+    dev = engine.DeviceGenome(w.contigs())
+    lens = [len(s) for _, s in w.contigs()]
+    rows, txs = [], []
+    for t in range(900):
+        n = int(rng.integers(1, 14))
+        b = len(rows)
+        for _ in range(n):
+            c = int(rng.integers(0, len(lens)))
+            ln = int(rng.integers(14, 21)) if t % 4 else int(rng.integers(40, 400))
+            st = int(rng.integers(0, lens[c] - ln))
+            rows.append(((st | (1 << 63)) if rng.integers(0, 2) else st, c, ln))
+        txs.append((b, n, 0))
+    ex = np.array(rows, dtype=engine.EXON_DTYPE)
+    tx = np.array(txs, dtype=engine.TX_DTYPE)
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    nuc, noff, _, _ = plan.run()
+    contigs = [s for _, s in w.contigs()]
+    for r, (b, n, _) in enumerate(txs):  # the records, gathered in Python (genome.py:603-614)
+        segs = []
+        for sr, c, ln in rows[b:b + n]:
+            s = contigs[c][sr & ~(1 << 63):(sr & ~(1 << 63)) + ln].decode('latin-1')
+            segs.append(mo.reverse_complement(s) if sr >> 63 else s)
+        assert nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1') == ''.join(segs)
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    raw = out.tobytes().decode('latin-1')
+    for r in range(len(tx)):
+        s = nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1')
+        want = _oracle_six(s)
+        for k in range(6):
+            j = 6 * r + k
+            t = raw[int(soff[j]):int(soff[j] + slen[j])]
+            if k < 2 and t[:1] == 'X':
+                t = t[1:]
+            assert t == (want[k] or ''), (r, k)
+    o6.close()
+    plan.close()
+    dev.close()
+
+
 # ---------------------------------------------------------------------------
 # FASTA text assembly on device (magot_fasta_text_*, SURVEY 8(f)2)
 # ---------------------------------------------------------------------------
