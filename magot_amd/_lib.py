@@ -12,7 +12,8 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libmagot.so')
+# MAGOT_LIB: an alternative build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get('MAGOT_LIB') or os.path.join(HERE, 'libmagot.so')
 
 OUT_NUC = 1
 OUT_PEP = 2

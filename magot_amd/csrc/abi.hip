@@ -536,12 +536,12 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     if (T1 < T0 + kChunk) T1 = std::min<uint64_t>(T0 + kChunk, B);
     const uint64_t dec_end = std::min<uint64_t>(T1 + kHalo, B);
     // residues owned: every codon starting before T1, rounded up to a chunk,
-    // but only codons that end inside the decoded range and at most 64 chunks
+    // but only codons that end inside the decoded range and at most kPepSlots chunks
     uint64_t R1 = P;
     if (T1 < B) {
       R1 = std::min<uint64_t>((pcount(T1) + kChunk - 1) & ~(uint64_t)(kChunk - 1), P);
       R1 = std::min<uint64_t>(R1, pcount(dec_end - 2));
-      R1 = std::min<uint64_t>(R1, (R0 & ~(uint64_t)(kChunk - 1)) + 64 * kChunk);
+      R1 = std::min<uint64_t>(R1, (R0 & ~(uint64_t)(kChunk - 1)) + kPepSlots * kChunk);
     }
     if (R1 < R0) R1 = R0;
     if (e2 < e1) e2 = e1;

@@ -81,15 +81,16 @@ void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out);
 constexpr int kThreads = 256;                 // one workgroup = 4 independent waves
 constexpr int kWaves = kThreads / 64;
 constexpr int kChunk = 16;                    // bytes per lane-store
-constexpr int kLaneChunks = 3;                // chunk slots per lane per tile
-constexpr int kSlots = 64 * kLaneChunks;      // 192 chunk slots per wave tile
-constexpr int kTile = 189 * kChunk;           // 3024 output bytes per tile: <= 1008 residues,
-                                              // so <= 64 residue chunks (one per lane)
+constexpr int kLaneChunks = 4;                // chunk slots per lane per tile
+constexpr int kSlots = 64 * kLaneChunks;      // 256 chunk slots per wave tile
+constexpr int kTile = (kSlots - 3) * kChunk;  // 4048 output bytes per tile (3 slots of halo):
+                                              // <= 1350 residues, <= 86 residue chunks
+constexpr int kPepPerLane = 2;                // residue chunk slots per lane
 constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
                                               // the residues rounded up to a 16-byte store
-constexpr int kExonCap = 128;                 // intervals staged in LDS per tile
+constexpr int kExonCap = 112;                 // intervals staged in LDS per tile (8 blocks of 4 waves fit a CU's LDS)
 constexpr int kTxCap = 64;                    // records staged in LDS per tile
-constexpr int kPepSlots = 64;                 // residue chunks per tile
+constexpr int kPepSlots = 64 * kPepPerLane;  // residue chunks per tile
 constexpr uint64_t kExcBit = 1ull << 62;      // interval touches an exception run
 
 // Debug switches carried in ExtractArgs.outputs (env MAGOT_DEBUG_PATHS):

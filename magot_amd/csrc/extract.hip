@@ -286,8 +286,9 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
                                       uint64_t span, int lane) {
   const int m = (int)d.m, nt = (int)d.nt;
 #pragma unroll
-  for (int h = 0; h < 3; ++h) codes[lane + 64 * h] = 0;
-  valid32[lane] = 0;
+  for (int h = 0; h < kLaneChunks; ++h) codes[lane + 64 * h] = 0;
+#pragma unroll
+  for (int h = 0; h < kPepPerLane; ++h) valid32[lane + 64 * h] = 0;
   __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -321,17 +322,22 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
     }
   }
   __builtin_amdgcn_wave_barrier();
-  const uint32_t h0 = codes[3 * lane], h1 = codes[3 * lane + 1], h2 = codes[3 * lane + 2];
-  const uint32_t p0 = valid32[lane];
-  const uint32_t c1 = h0 + h1, c2 = c1 + h2;
+  // lane l scans chunk slots kLaneChunks*l .. and residue chunks
+  // kPepPerLane*l .. (inclusive running counts)
+  uint32_t hc[kLaneChunks], pc[kPepPerLane];
+#pragma unroll
+  for (int i = 0; i < kLaneChunks; ++i) hc[i] = codes[kLaneChunks * lane + i] + (i ? hc[i - 1] : 0u);
+#pragma unroll
+  for (int i = 0; i < kPepPerLane; ++i) pc[i] = valid32[kPepPerLane * lane + i] + (i ? pc[i - 1] : 0u);
+  const uint32_t ct = hc[kLaneChunks - 1], pt = pc[kPepPerLane - 1];
   // both scans in one: interval counts (<= kExonCap) low, record counts high
-  const uint32_t sc = wave_scan(c2 | (p0 << 16));
-  const uint32_t cx = (sc & 0xFFFFu) - c2;
-  const uint32_t px = sc >> 16;
-  L.cmap[3 * lane] = (uint8_t)(cx + h0);
-  L.cmap[3 * lane + 1] = (uint8_t)(cx + c1);
-  L.cmap[3 * lane + 2] = (uint8_t)(cx + c2);
-  L.pmap[lane] = (uint8_t)px;
+  const uint32_t sc = wave_scan(ct | (pt << 16));
+  const uint32_t cx = (sc & 0xFFFFu) - ct;
+  const uint32_t px = (sc >> 16) - pt;
+#pragma unroll
+  for (int i = 0; i < kLaneChunks; ++i) L.cmap[kLaneChunks * lane + i] = (uint8_t)(cx + hc[i]);
+#pragma unroll
+  for (int i = 0; i < kPepPerLane; ++i) L.pmap[kPepPerLane * lane + i] = (uint8_t)(px + pc[i]);
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -467,9 +473,9 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   }
   __builtin_amdgcn_wave_barrier();
 
-  // ---- translation: one residue chunk per lane ----------------------------
-  const int c = lane;
-  if (c >= g.n_pc) return;
+  // ---- translation: kPepPerLane residue chunks per lane --------------------
+#pragma unroll 1
+  for (int c = lane; c < g.n_pc; c += 64) {
   const int q_first = c * 16 - g.qshift;  // residue of slot 0 (rel Q0)
   const int kk0 = c == 0 ? g.qshift : 0;
   const int kk1 = min(16, g.n_res - q_first);
@@ -561,6 +567,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)
       if (kk >= kk0 && kk < kk1) pdst[kk] = (uint8_t)(w[kk >> 2] >> (8 * (kk & 3)));
+  }
   }
 }
 
