@@ -481,7 +481,15 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
       // does [gs, gs+len) touch an exception run?  (dir: first run ending past the block)
       uint64_t d = g->host_dir[gs >> kDirShift] & ~kDirClean;
       while (g->host_runs[d].start + g->host_runs[d].len <= gs) ++d;
-      const uint64_t exc = g->host_runs[d].start < gs + x.len ? kExcBit : 0;
+      uint64_t exc = g->host_runs[d].start < gs + x.len ? kExcBit : 0;
+      if (exc && !(x.start_rc & kRcBit)) {
+        // forward strand: a byte without a literal class needs the run list
+        for (uint64_t r = d; g->host_runs[r].start < gs + x.len; ++r)
+          if (lit_class(g->host_runs[r].byte) == 7u) {
+            exc |= kSlowLitBit;
+            break;
+          }
+      }
       ex_g.push_back(gs | (x.start_rc & kRcBit) | exc);
       ex_out.push_back(acc);
       acc += x.len;
@@ -1023,7 +1031,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   std::vector<uint64_t> starts(ne + 1);
   for (uint64_t i = 0; i < ne; ++i) {
     const uint64_t gw = ex_g[i], o0 = ex_out[i], len = ex_out[i + 1] - o0;
-    const uint64_t gs = gw & ~(kRcBit | kExcBit);
+    const uint64_t gs = gw & ~kExFlagBits;
     rows[2 * i] = (gw & kRcBit) ? 2 * span - gs - len - o0 : gs - o0;
     rows[2 * i + 1] = o0 | ((gw & kExcBit) ? kOrf6ExcRow : 0ull);  // the exact path's flag
     starts[i] = o0;

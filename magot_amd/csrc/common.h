@@ -92,6 +92,21 @@ constexpr int kExonCap = 112;                 // intervals staged in LDS per til
 constexpr int kTxCap = 64;                    // records staged in LDS per tile
 constexpr int kPepSlots = 64 * kPepPerLane;  // residue chunks per tile
 constexpr uint64_t kExcBit = 1ull << 62;      // interval touches an exception run
+constexpr uint64_t kSlowLitBit = 1ull << 61;  // ... whose byte has no literal class (below)
+constexpr uint64_t kExFlagBits = kRcBit | kExcBit | kSlowLitBit;
+
+// Exception bases carry a literal class in their nibble's low three bits
+// (nibble = 8 | class): the bytes the kernels can write without the run
+// list.  Forward strand: N n - R Y K M; any other byte is class 7 and its
+// intervals take the run-list path.  The reverse-strand mirror holds the
+// class of the reverse-complement literal (genome.py:787,792: N, n, - kept,
+// everything else becomes n), which is always 0, 1 or 2.
+__host__ __device__ constexpr uint32_t lit_class(uint32_t b) {
+  return b == 'N' ? 0u : b == 'n' ? 1u : b == '-' ? 2u : b == 'R' ? 3u : b == 'Y' ? 4u
+       : b == 'K' ? 5u : b == 'M' ? 6u : 7u;
+}
+constexpr uint32_t kLitLo = 0x522D6E4Eu;  // classes 0..3: N n - R (little-endian bytes)
+constexpr uint32_t kLitHi = 0x4E4D4B59u;  // classes 4..7: Y K M (7: never written from here)
 
 // Debug switches carried in ExtractArgs.outputs (env MAGOT_DEBUG_PATHS):
 // force the general per-segment / per-residue paths.

@@ -50,7 +50,8 @@ struct WaveLds {
 };
 
 constexpr uint32_t kFlagRc = 1u;
-constexpr uint32_t kFlagExc = 2u;
+constexpr uint32_t kFlagExc = 2u;      // touches an exception run
+constexpr uint32_t kFlagSlowLit = 4u;  // ... one without a literal class (run-list path)
 
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
   return __builtin_amdgcn_alignbit(hi, lo, sh);  // (hi:lo >> sh)[31:0], sh in 0..31
@@ -119,6 +120,45 @@ __device__ __forceinline__ uint4 chunk_ascii(uint32_t x0, uint32_t x1, uint32_t 
     }
   }
   return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// As chunk_ascii, for chunks that may hold exception nibbles (8 | literal
+// class): a second 8-entry table gives N n - R Y K M, selected per byte by
+// the exception bit.
+__device__ __forceinline__ uint4 chunk_ascii_lit(uint32_t x0, uint32_t x1, uint32_t exc,
+                                                 const uint32_t lit[4]) {
+  uint32_t s[4];
+  spread_nibbles(x0, s[0], s[1]);
+  spread_nibbles(x1, s[2], s[3]);
+  uint32_t w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t base = __builtin_amdgcn_perm(0x74676361u, 0x54474341u, s[q] & 0x07070707u);
+    const uint32_t lits = __builtin_amdgcn_perm(kLitHi, kLitLo, s[q] & 0x07070707u);
+    const uint32_t m = ((s[q] >> 3) & 0x01010101u) * 0xFFu;
+    w[q] = bfi(m, lits, base);
+  }
+  if (exc) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t b01 = spread_bits((exc >> (4 * q)) & 0xFu);
+      const uint32_t em = (b01 << 8) - b01;
+      w[q] = (w[q] & ~em) | (lit[q] & em);
+    }
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// The exception bits (nibble bit 3) of 16 nibbles as a 16-bit mask.
+__device__ __forceinline__ uint32_t exc_bits(uint32_t x0, uint32_t x1) {
+  uint32_t e0 = (x0 >> 3) & 0x11111111u, e1 = (x1 >> 3) & 0x11111111u;
+  e0 = (e0 | (e0 >> 3)) & 0x03030303u;
+  e1 = (e1 | (e1 >> 3)) & 0x03030303u;
+  e0 = (e0 | (e0 >> 6)) & 0x000F000Fu;
+  e1 = (e1 | (e1 >> 6)) & 0x000F000Fu;
+  e0 = (e0 | (e0 >> 12)) & 0xFFu;
+  e1 = (e1 | (e1 >> 12)) & 0xFFu;
+  return e0 | (e1 << 8);
 }
 
 // 16 nibbles -> 16 packed 2-bit codes (base k at bits 2k) for translation.
@@ -296,14 +336,15 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
     if (j < m) {
       const uint64_t o0 = rows.o0[h], o1 = rows.o1[h], gw = rows.g[h];
       const bool rc = (gw & kRcBit) != 0;
-      const uint64_t gs = gw & ~(kRcBit | kExcBit);
+      const uint64_t gs = gw & ~kExFlagBits;
       const int64_t s = (int64_t)(o0 - d.T0);
       const int64_t e = (int64_t)(o1 - d.T0);
       // chunk byte p of the tile reads unified base U + p: forward g = gs + (p - s),
       // reverse strand 2*span-1 - (gs + len-1 - (p - s))
       const uint64_t U = rc ? 2 * span - gs - (o1 - o0) - (uint64_t)s : gs - (uint64_t)s;
       const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
-      const uint32_t fl = (rc ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u);
+      const uint32_t fl = (rc ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u) |
+                          ((gw & kSlowLitBit) ? kFlagSlowLit : 0u);
       L.ex[j] = make_uint4((uint32_t)U, (uint32_t)(U >> 32), end32, fl);
       if (j >= 1) {
         const int cj = ((int)s + kChunk - 1) / kChunk;
@@ -424,7 +465,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     const bool two = n1 < cend - p;
     const uint64_t wa = UA + (uint64_t)p;
     const uint64_t wb = two ? UB + (uint64_t)p : wa;
-    const bool slow = ((X.w | (two ? Y.w : 0u)) & kFlagExc) != 0 || (two && (int)Y.z < cend) ||
+    const bool slow = ((X.w | (two ? Y.w : 0u)) & kFlagSlowLit) != 0 || (two && (int)Y.z < cend) ||
                       (a.outputs & kDebugSlowNuc);
     meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (slow ? 16u : 0u) |
               ((uint32_t)(wa & 7) << 8) | ((uint32_t)(wb & 7) << 16) |
@@ -435,10 +476,16 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   uint32_t x0k[kLaneChunks], x1k[kLaneChunks];
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) fast_chunk(wA[k], wB[k], meta[k], x0k[k], x1k[k]);
-  uint32_t slow_any = 0;
+  uint32_t slow_any = 0, exc_any = 0;
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) slow_any |= meta[k] & 16u;
+  for (int k = 0; k < kLaneChunks; ++k) {
+    slow_any |= meta[k] & 16u;
+    exc_any |= (meta[k] & 1u) ? (x0k[k] | x1k[k]) & 0x88888888u : 0u;
+  }
   const bool any_slow = __builtin_amdgcn_readfirstlane(__ballot(slow_any != 0) != 0);
+  // exception nibbles on the fast path (N runs, IUPAC with a literal class):
+  // the wave decodes them from the nibble, without the run list
+  const bool any_exc = __builtin_amdgcn_readfirstlane(__ballot(exc_any != 0) != 0);
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) {
     const int c = lane + 64 * k;
@@ -459,10 +506,11 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     }
     if (mt & 1u) {
       if (want_nuc && c < g.n_out)
-        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) = chunk_ascii(x0k[k], x1k[k], ex, lit);
+        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) =
+            any_exc ? chunk_ascii_lit(x0k[k], x1k[k], ex, lit) : chunk_ascii(x0k[k], x1k[k], ex, lit);
       if (want_pep) {
         codes[c] = pack_codes(x0k[k], x1k[k]);
-        valid16[c] = (uint16_t)~ex;
+        valid16[c] = (uint16_t)~(any_exc ? (ex | exc_bits(x0k[k], x1k[k])) : ex);
       }
     }
   }
@@ -577,8 +625,16 @@ __global__ __launch_bounds__(256) void mirror_planes_kernel(uint32_t* __restrict
   // the codes complemented (soft-mask and exception bits kept)
   const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (w >= nw) return;
-  const uint32_t x = __builtin_bswap32(nib[nw - 1 - w]);
-  nib[nw + w] = (((x >> 4) & 0x0F0F0F0Fu) | ((x << 4) & 0xF0F0F0F0u)) ^ 0x33333333u;
+  const uint32_t b = __builtin_bswap32(nib[nw - 1 - w]);
+  const uint32_t x = ((b >> 4) & 0x0F0F0F0Fu) | ((b << 4) & 0xF0F0F0F0u);
+  // exception nibbles (8 | class): class of the reverse-complement literal,
+  // N n - kept (0 1 2), every other class becomes n (1)
+  const uint32_t e = (x >> 3) & 0x11111111u;
+  const uint32_t emask = e * 0xFu;
+  const uint32_t cls = x & 0x77777777u;
+  const uint32_t big = ((cls + 0x55555555u) >> 3) & 0x11111111u;  // class >= 3
+  const uint32_t rc = (cls & ~(big * 7u)) | big;
+  nib[nw + w] = ((x ^ 0x33333333u) & ~emask) | ((0x88888888u | rc) & emask);
 }
 
 }  // namespace

@@ -16,11 +16,11 @@ namespace magot {
 namespace {
 
 struct ByteClass {
-  uint8_t nib[256];    // nibble for ACGTacgt, 8 (exception) otherwise
+  uint8_t nib[256];    // nibble for ACGTacgt, 8 | lit_class (exception) otherwise
   uint8_t plain[256];  // 1 for ACGTacgt
   ByteClass() {
     for (int i = 0; i < 256; ++i) {
-      nib[i] = 8;
+      nib[i] = (uint8_t)(8u | lit_class((uint32_t)i));
       plain[i] = 0;
     }
     const char up[4] = {'A', 'C', 'G', 'T'};
