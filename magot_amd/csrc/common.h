@@ -81,10 +81,10 @@ void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out);
 constexpr int kThreads = 256;                 // one workgroup = 4 independent waves
 constexpr int kWaves = kThreads / 64;
 constexpr int kChunk = 16;                    // bytes per lane-store
-constexpr int kLaneChunks = 4;                // chunk slots per lane per tile
-constexpr int kSlots = 64 * kLaneChunks;      // 256 chunk slots per wave tile
-constexpr int kTile = (kSlots - 3) * kChunk;  // 4048 output bytes per tile (3 slots of halo):
-                                              // <= 1350 residues, <= 86 residue chunks
+constexpr int kLaneChunks = 5;                // chunk slots per lane per tile
+constexpr int kSlots = 64 * kLaneChunks;      // 320 chunk slots per wave tile
+constexpr int kTile = (kSlots - 3) * kChunk;  // 5072 output bytes per tile (3 slots of halo):
+                                              // <= 1691 residues, <= 106 residue chunks
 constexpr int kPepPerLane = 2;                // residue chunk slots per lane
 constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
                                               // the residues rounded up to a 16-byte store
