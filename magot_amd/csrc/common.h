@@ -88,7 +88,7 @@ constexpr int kTile = (kSlots - 3) * kChunk;  // 5072 output bytes per tile (3 s
 constexpr int kPepPerLane = 2;                // residue chunk slots per lane
 constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
                                               // the residues rounded up to a 16-byte store
-constexpr int kExonCap = 112;                 // intervals staged in LDS per tile (8 blocks of 4 waves fit a CU's LDS)
+constexpr int kExonCap = 128;                 // intervals staged in LDS per tile (7 blocks of 4 waves fit a CU's LDS)
 constexpr int kTxCap = 64;                    // records staged in LDS per tile
 constexpr int kPepSlots = 64 * kPepPerLane;  // residue chunks per tile
 constexpr uint64_t kExcBit = 1ull << 62;      // interval touches an exception run
