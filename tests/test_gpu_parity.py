@@ -456,6 +456,48 @@ def test_orf6_fused_gather_tiny_intervals_vs_oracle():
     dev.close()
 
 
+def test_every_byte_class_both_strands_vs_oracle():
+    """Every printable byte GenomeSequence keeps (genome.py:875) inside CDS
+    intervals on both strands: the literal classes the kernels decode from
+    the nibble (N n - R Y K M; forward strand) and the run-list path (every
+    other byte; reverse strand maps all of them to n N -)."""
+    rng = np.random.default_rng(71)
+    printable = bytes(range(33, 127)) + b' '
+    contig = bytearray(rng.choice(np.frombuffer(b'ACGTacgt', np.uint8), 60_000).tobytes())
+    for k in range(0, 60_000, 400):  # a run of one byte class every 400 bases
+        b = printable[(k // 400) % len(printable)]
+        contig[k:k + 1 + (k // 400) % 37] = bytes([b]) * (1 + (k // 400) % 37)
+    contig = bytes(contig)
+    dev = engine.DeviceGenome([('c0', contig)])
+    rows, txs = [], []
+    for t in range(600):
+        n = int(rng.integers(1, 6))
+        b = len(rows)
+        minus = bool(rng.integers(0, 2))
+        for _ in range(n):
+            ln = int(rng.integers(1, 300))
+            st = int(rng.integers(0, len(contig) - ln))
+            rows.append(((st | (1 << 63)) if minus else st, 0, ln))
+        txs.append((b, n, 0))
+    ex = np.array(rows, dtype=engine.EXON_DTYPE)
+    tx = np.array(txs, dtype=engine.TX_DTYPE)
+    plan = engine.ExtractionPlan(dev, ex, tx)
+    nuc, noff, pep, poff = plan.run()
+    text = contig.decode('latin-1')
+    for r, (b, n, _) in enumerate(txs):
+        segs = []
+        for sr, _c, ln in rows[b:b + n]:
+            st = sr & ~(1 << 63)
+            s = text[st:st + ln]
+            segs.append(mo.reverse_complement(s) if sr >> 63 else s)
+        want = ''.join(segs)
+        assert nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1') == want, r
+        got = pep[int(poff[r]):int(poff[r + 1])].tobytes().decode('latin-1')
+        assert got == (mo.translate(want, trimX=False) or ''), r
+    plan.close()
+    dev.close()
+
+
 def test_orf6_fused_code_plane_boundaries_vs_oracle():
     """The fused gather's 2-bit fast path at its edges: intervals of 14-20
     bases put the second (and third) interval exactly at the 16th-18th
