@@ -123,18 +123,19 @@ def cpu_baseline(w, budget_bases, orfs=False):
     t0 = time.perf_counter()
     nucs = [mo.get_fasta(r, aset, 'nucleotide') for r in recs]
     t1 = time.perf_counter()
+    protein = w.outputs != 'nuc'  # C2 is extraction only (BASELINE configs[1])
     if orfs:
         for text in nucs:
             mo.get_orfs(text.split('\n', 1)[1])
-    else:
+    elif protein:
         for r in recs:
             mo.get_fasta(r, aset, 'protein')
     t2 = time.perf_counter()
     rate = bases / (t2 - t0)
-    second = 'get_orfs (six frames)' if orfs else 'protein'
+    second = 'get_orfs (six frames)' if orfs else ('protein' if protein else 'no translation')
     cal = None
     cal_path = os.path.join(ROOT, 'profiles', 'cpu_calibration.json')
-    if os.path.exists(cal_path) and not orfs:  # calibrated on nucleotide + protein only
+    if os.path.exists(cal_path) and not orfs and protein:  # calibrated on nucleotide + protein
         with open(cal_path) as fh:
             ratio = json.load(fh)['port_over_reference_mean']
         # the reference's own loop (AnnotationSet.__getitem__ evals, genome.py:536-544)
