@@ -12,22 +12,25 @@
 //
 // Work decomposition (output-stationary, HBM-bound):
 //   * The host cuts the concatenated nucleotide output into 16-byte aligned
-//     tiles of <= 3024 bytes (189 chunks of 16 bytes; shorter where a tile
-//     would touch more than kExonCap intervals or kTxCap records).  A tile
-//     belongs to ONE wavefront: 64 lanes x 3 chunk slots (189 output chunks +
-//     a halo chunk for codons that run past the tile end), so there is no
-//     workgroup barrier (every wave writes its own copy of the codon table).
+//     tiles of <= kTile = 5072 bytes (317 chunks of 16 bytes; shorter where a
+//     tile would touch more than kExonCap intervals or kTxCap records).  A
+//     tile belongs to ONE wavefront: 64 lanes x 5 chunk slots (317 output
+//     chunks + a 3-chunk halo for codons that run past the tile end) and 1-2
+//     residue chunks per lane, so there is no workgroup barrier (every wave
+//     writes its own copy of the codon table).
 //   * Staging: the tile's intervals go to wave-private LDS as {64-bit unified
 //     anchor, tile-relative end, flags}; chunk -> interval and residue chunk
 //     -> record maps come from an LDS histogram + one packed DPP wave scan.
-//   * The genome is a nibble plane (code | soft-mask << 2 | exception << 3)
-//     followed by its reverse-complement mirror, so a '-' interval reads its
-//     strand forward exactly like a '+' interval.  A chunk is at most two
-//     interval segments on the fast path: one buffer_load_dwordx3 window per
-//     segment, two funnel shifts, a nibble-mask merge, v_perm nibble spread +
-//     v_perm ASCII table, one 16-byte store.  Intervals that touch an
-//     exception run (N, IUPAC ...; flagged per interval by the host) and
-//     chunks over 3+ intervals take build_chunk_slow.
+//   * The genome is a nibble plane (code | soft-mask << 2, or 8 | literal
+//     class for an exception byte) followed by its reverse-complement mirror,
+//     so a '-' interval reads its strand forward exactly like a '+' interval.
+//     A chunk is at most two interval segments on the fast path: one
+//     buffer_load_dwordx3 window per segment, two funnel shifts, a nibble-mask
+//     merge, v_perm nibble spread + v_perm ASCII table (a second table for the
+//     literal classes N n - R Y K M when the wave holds exception nibbles),
+//     one 16-byte store.  Intervals over a byte without a literal class
+//     (flagged per interval by the host) and chunks over 3+ intervals take
+//     build_chunk_slow, which patches literals from the run list.
 //   * 2-bit codes and validity bits of the tile stay in LDS; a residue chunk
 //     funnel-shifts 48 bases of codes out of LDS per record segment (<= 2 on
 //     the fast path), looks the 16 codons up in a 64-byte LDS table and
