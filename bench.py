@@ -149,6 +149,48 @@ def cpu_baseline(w, budget_bases, orfs=False):
                                                    second, t2 - t1)}
 
 
+def cpu_c_port(w, threads):
+    """A stronger CPU reference point: the C restatement
+    of the same per-record loop (oracle/cds_oracle.c) over the WHOLE
+    workload, records split into `threads` contiguous slices run in parallel
+    (ctypes releases the GIL).  Only the C calls are timed."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import cds_oracle
+    cds_oracle.lib().oracle_extract  # load (and build) before the threads start
+    first = np.zeros(w.n_tx + 1, dtype=np.int64)
+    np.cumsum(w.ex_count, out=first[1:])
+    protein = w.outputs != 'nuc'
+    bounds = np.linspace(0, w.n_tx, threads + 1).astype(np.int64)
+    jobs = []
+    for i in range(threads):
+        t0, t1 = int(bounds[i]), int(bounds[i + 1])
+        e0, e1 = int(first[t0]), int(first[t1])
+        counts = w.ex_count[t0:t1]
+        rec_off = np.zeros(t1 - t0 + 1, dtype=np.int64)
+        np.cumsum(counts, out=rec_off[1:])
+        tx_of = np.repeat(np.arange(t0, t1), counts)
+        c0 = w.ex_start[e0:e1] + 1
+        c1 = w.ex_start[e0:e1] + w.ex_len[e0:e1]
+        sk = np.where(w.tx_strand[tx_of] < 0, ord('-'), ord('+')).astype(np.uint8)
+        jobs.append((rec_off, w.tx_contig[tx_of], c0, c1, sk))
+
+    def run(job, prot):
+        return cds_oracle.extract(w.genome, w.contig_off, job[0], job[1], job[2], job[3], job[4],
+                                  prot)
+
+    with ThreadPoolExecutor(threads) as ex:
+        t0 = time.perf_counter()
+        list(ex.map(lambda j: run(j, False), jobs))
+        t1 = time.perf_counter()
+        if protein:
+            list(ex.map(lambda j: run(j, True), jobs))
+        t2 = time.perf_counter()
+    return {'value': w.cds_bases / (t2 - t0), 'unit': 'bases/s', 'cores': threads,
+            'kind': 'port (C)',
+            'sample': 'whole workload, %d threads; nucleotide %.3fs%s; oracle/cds_oracle.c'
+                      % (threads, t1 - t0, (' + protein %.3fs' % (t2 - t1)) if protein else '')}
+
+
 def strong_main(args, dist, rank, local, world):
     """C4: the single C3 job on `world` GPUs.
 
@@ -463,6 +505,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log('timing the CPU baseline on a bounded sample ...')
         cpu = cpu_baseline(w, args.cpu_sample_bases)
+        # the host cores this GPU's share of the box has (16 per GPU on the pool)
+        threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
+        cpu['c_port_all_cores'] = cpu_c_port(w, threads)
 
     if rank == 0:
         desc = {'C3': '1 Gb genome (64 lognormal contigs) + 500k transcripts x (1+Poisson(7)) '
