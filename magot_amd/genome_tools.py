@@ -7,6 +7,8 @@
     python -m magot_amd.genome_tools extract_upstream_downstream <fasta> <gff> <length> up|down
            [feature_type=gene] [namefrom=ID] [truncate_names=True]
     python -m magot_amd.genome_tools coords2fasta <fasta> <seqid> <start> <stop> [truncate_names=False]
+    python -m magot_amd.genome_tools dna2orfs <fasta> <output_file>   (broken in the reference:
+           TypeError, reproduced)
 
 Arguments follow the reference's CLI convention (genome_tools.py:25-45):
 positional values, then ``key=value`` pairs, all strings.  The reference
@@ -225,9 +227,24 @@ def coords2fasta(fasta_file, seqid, start, stop, truncate_names='False'):
     _write(_gather(seqs, [(index[seqid], st, ln, False)])[0] + '\n')
 
 
+def dna2orfs(fasta_location, output_file, from_atg=False, longest=False):
+    """genome_tools.py:145-180.  The reference builds a Genome, opens
+    output_file for writing and then calls ``.translate(frame=, strand=)`` on
+    each contig's plain ``str`` (GenomeSequence values are str,
+    genome.py:870-877): that is ``str.translate``, which takes no keyword
+    arguments, so with at least one contig it raises TypeError and leaves the
+    output file empty -- on Python 2.7 as here (tests/golden/orfs.json, from
+    the reference).  Reproduced as is; the working six-frame path is
+    ``Sequence.get_orfs`` (orf6_kernel)."""
+    dna = genome.Genome(fasta_location)
+    with open(output_file, 'w'):
+        for _ in dna.genome_sequence:
+            raise TypeError('translate() takes no keyword arguments')
+
+
 TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep,
          'extract_upstream_downstream': extract_upstream_downstream,
-         'coords2fasta': coords2fasta}
+         'coords2fasta': coords2fasta, 'dna2orfs': dna2orfs}
 
 
 def parse_argv(argv):
