@@ -151,12 +151,13 @@ __global__ __launch_bounds__(kOpsThreads) void translate_kernel(
 //
 // Output layout: every stream starts on a 16-byte boundary (soff holds the
 // padded offsets, the real lengths follow from the record length); the
-// residues of a 16-byte chunk past the stream's end repeat its last residue.
+// bytes of a stream's last 16-byte chunk past its end are zero.
 //
 // Input-stationary: one wave owns a tile of kOrfTile bases of the
 // concatenated records and every output chunk whose first codon starts in
 // it (all six streams of every record the tile touches).  The tile plus a
-// 48/50-base halo is staged once, as one byte per position:
+// 48/50-base halo is staged once (over the genome: computed in registers
+// from the 2-bit code and 1-bit exception planes), as one byte per position:
 //   cidx[p] = c[p] | c[p+1] << 2 | c[p+2] << 4 | (any of the three not
 //             ACGTacgt) << 6
 // so a '+' residue is tbl[cidx[p]] and a '-' residue (codon read backwards,
