@@ -173,6 +173,10 @@ __device__ __forceinline__ uint32_t pack_codes(uint32_t x0, uint32_t x1) {
   return __builtin_amdgcn_perm(z1, z0, 0x06040200u);
 }
 
+#ifndef MAGOT_EXP_LOAD_AUX
+#define MAGOT_EXP_LOAD_AUX 0  // cache-policy bits of the genome window loads
+#endif
+
 struct Planes {
   const uint32_t* __restrict__ nib;
   const uint32_t* __restrict__ dir;
@@ -396,7 +400,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* pla
 
 __device__ __forceinline__ uint3 load_window(__amdgpu_buffer_rsrc_t plane, uint64_t u) {
   const uint32_t off = __builtin_amdgcn_alignbit((uint32_t)(u >> 32), (uint32_t)u, 1) & ~3u;
-  const auto v = __builtin_amdgcn_raw_buffer_load_b96(plane, off, 0, 0);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b96(plane, off, 0, MAGOT_EXP_LOAD_AUX);
   return make_uint3(v[0], v[1], v[2]);
 }
 
@@ -509,8 +513,8 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     }
     if (mt & 1u) {
       if (want_nuc && c < g.n_out)
-        *reinterpret_cast<uint4*>(a.nuc + T0 + (uint64_t)p) =
-            any_exc ? chunk_ascii_lit(x0k[k], x1k[k], ex, lit) : chunk_ascii(x0k[k], x1k[k], ex, lit);
+        store16(a.nuc + T0 + (uint64_t)p,
+                any_exc ? chunk_ascii_lit(x0k[k], x1k[k], ex, lit) : chunk_ascii(x0k[k], x1k[k], ex, lit));
       if (want_pep) {
         codes[c] = pack_codes(x0k[k], x1k[k]);
         valid16[c] = (uint16_t)~(any_exc ? (ex | exc_bits(x0k[k], x1k[k])) : ex);
@@ -613,7 +617,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   }
   uint8_t* const pdst = a.pep + g.qbase + 16 * (uint64_t)c;
   if (kk0 == 0 && kk1 == 16) {
-    *reinterpret_cast<uint4*>(pdst) = make_uint4(w[0], w[1], w[2], w[3]);
+    store16(pdst, make_uint4(w[0], w[1], w[2], w[3]));
   } else {
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk)

@@ -283,7 +283,7 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
       o[j] &= (uint32_t)(0xFFFFFFFFull >> (8 * drop));
     }
   }
-  *reinterpret_cast<uint4*>(a.out + g.out0 + 16 * (uint64_t)q) = make_uint4(o[0], o[1], o[2], o[3]);
+  store16(a.out + g.out0 + 16 * (uint64_t)q, make_uint4(o[0], o[1], o[2], o[3]));
 }
 
 // kGenome = false: the records are bytes in a.nuc (Sequence.get_orfs batch).
