@@ -14,7 +14,7 @@ timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail 
 cat $OUT/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python bench.py --no-cpu-baseline > $OUT/kt.json 2> $OUT/kt.err || { tail -30 $OUT/kt.err; exit 1; }
 grep -h extract_kernel $OUT/kt/kt_kernel_stats.csv
-timeout -k 10 900 python bench.py --config C5 --steps 10 --warmup 2 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -30 $OUT/bench_c5.err; exit 1; }
+timeout -k 10 900 python bench.py --config C5 --steps 30 --warmup 10 > $OUT/bench_c5.json 2> $OUT/bench_c5.err || { tail -30 $OUT/bench_c5.err; exit 1; }
 cat $OUT/bench_c5.json
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt5 -o kt -- python bench.py --config C5 --steps 10 --warmup 2 --no-verify > $OUT/kt5.json 2> $OUT/kt5.err || { tail -30 $OUT/kt5.err; exit 1; }
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt5 -o kt -- python bench.py --config C5 --steps 30 --warmup 10 --no-verify > $OUT/kt5.json 2> $OUT/kt5.err || { tail -30 $OUT/kt5.err; exit 1; }
 grep -h "orf6\|extract_kernel" $OUT/kt5/kt_kernel_stats.csv

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
-BENCH="bench.py --steps 20 --warmup 3"
+BENCH="bench.py"
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m "gpu and not slow" -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
