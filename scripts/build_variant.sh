@@ -9,7 +9,7 @@ D=magot_amd/_build/var_$NAME; mkdir -p $D
 objs=""
 for f in magot_amd/_build/*.o; do
   b=$(basename $f)
-  if [ $b = extract.hip.o ] || [ $b = seqops.hip.o ]; then
+  if [ $b = extract.hip.o ] || [ $b = seqops.hip.o ] || [ $b = abi.hip.o ]; then
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 -Iinclude "$@" -x hip -c magot_amd/csrc/${b%.o} -o $D/$b
     objs="$objs $D/$b"
   else
