@@ -283,7 +283,7 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
       o[j] &= (uint32_t)(0xFFFFFFFFull >> (8 * drop));
     }
   }
-  store16(a.out + g.out0 + 16 * (uint64_t)q, make_uint4(o[0], o[1], o[2], o[3]));
+  *reinterpret_cast<uint4*>(a.out + g.out0 + 16 * (uint64_t)q) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
 // kGenome = false: the records are bytes in a.nuc (Sequence.get_orfs batch).
@@ -312,7 +312,16 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     s_code[threadIdx.x] = (uint8_t)(c < 4 ? c : 0x40u);
     __syncthreads();
   }
-  const uint64_t tile = (uint64_t)blockIdx.x * (kOpsThreads / 64) + wave;
+  // XCD-aware tile order: blocks are dealt round-robin to the 8 XCDs, so
+  // virtual block vb gives each XCD one contiguous run of tiles.  A record
+  // cut by a tile boundary leaves a partial 128-byte line in each of its six
+  // streams; with both tiles on one XCD the two halves merge in that XCD's
+  // L2.  Together with plain (not non-temporal) stores here: WRITE_SIZE 5.26
+  // -> 5.06 GB per launch, C5 step 1.72 -> 1.65 ms (A/B, one box, medians).
+  const uint32_t xnb = gridDim.x, xb = blockIdx.x;
+  const uint32_t xq = xnb >> 3, xr = xnb & 7, xcd = xb & 7, xk = xb >> 3;
+  const uint32_t vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  const uint64_t tile = (uint64_t)vb * (kOpsThreads / 64) + wave;
   if (tile >= a.n_tiles) return;  // wave-uniform
   s_tblw[lane] = reinterpret_cast<const uint32_t*>(a.tables)[lane];
   const uint8_t* const s_tbl = reinterpret_cast<const uint8_t*>(s_tblw);
