@@ -1,0 +1,23 @@
+#!/bin/bash
+# Diagnostic: does extra VALU work cost more back-to-back than in isolated
+# launches?  (kernel trace of 200 back-to-back steps + 20 isolated launches)
+# Needs scripts/experiments/dummy_valu.patch applied, then
+#   scripts/build_variant.sh valu -DMAGOT_EXP_DUMMY_VALU=100 and lib_base.so = the plain build.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out/valu; rm -rf $OUT; mkdir -p $OUT
+for v in base valu base valu; do
+  rm -rf $OUT/$v
+  MAGOT_LIB=$PWD/scripts/lib_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/$v -o kt -- python bench.py --steps 200 --warmup 20 --no-verify --no-cpu-baseline > $OUT/$v.json 2> $OUT/$v.err || { tail -5 $OUT/$v.err; exit 1; }
+  python3 - $v <<'PY'
+import csv, glob, sys, json
+v = sys.argv[1]
+rows = [r for f in glob.glob('gpurun_out/valu/%s/**/*kernel_trace.csv' % v, recursive=True)
+        for r in csv.DictReader(open(f)) if 'extract_kernel' in r['Kernel_Name']]
+rows.sort(key=lambda r: int(r['Start_Timestamp']))
+d = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6 for r in rows]
+b2b, iso = d[21:221], d[-20:]
+print(v, 'b2b %.4f' % (sum(b2b) / len(b2b)), 'isolated %.4f' % (sum(iso) / len(iso)))
+PY
+done
