@@ -17,7 +17,9 @@ rows = [r for f in glob.glob('gpurun_out/valu/%s/**/*kernel_trace.csv' % v, recu
         for r in csv.DictReader(open(f)) if 'extract_kernel' in r['Kernel_Name']]
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 d = [(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e6 for r in rows]
-b2b, iso = d[21:221], d[-20:]
+W, S = 20, 200  # bench --warmup 20 --steps 200 --no-verify: W warm-up, S back-to-back, 20 isolated
+assert len(d) == W + S + 20, len(d)
+b2b, iso = d[W:W + S], d[W + S:]
 print(v, 'b2b %.4f' % (sum(b2b) / len(b2b)), 'isolated %.4f' % (sum(iso) / len(iso)))
 PY
 done
