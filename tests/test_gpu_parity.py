@@ -331,6 +331,33 @@ def test_sorted_record_order_vs_c_oracle():
     check_against_oracle(w)
 
 
+def _recase(w, rng, lo, hi):
+    """Soft-mask runs of U[lo, hi] bases (alternating case) over the plain
+    bases of w's genome; exception bytes are left as they are."""
+    g = w.genome
+    n = len(g)
+    runs = rng.integers(lo, hi + 1, size=n // lo + 2)
+    ends = np.cumsum(runs)
+    lower = np.zeros(n, dtype=bool)
+    lower_run = np.searchsorted(ends, np.arange(n), side='right') & 1
+    lower[:] = lower_run.astype(bool)
+    plain = np.isin(g, np.frombuffer(b'ACGTacgt', dtype=np.uint8))
+    up = g & 0xDF
+    w.genome = np.where(plain, np.where(lower, up | 0x20, up), g).astype(np.uint8)
+    return w
+
+
+@pytest.mark.parametrize('runs', [(1, 40), (10, 30), (150, 600)])
+def test_dense_soft_mask_runs_vs_c_oracle(runs):
+    """Soft-mask runs of 1-600 bases (case changes inside chunks, at chunk
+    edges and across interval joins), intervals of 1-400 bases, both
+    strands, N runs and IUPAC bytes."""
+    rng = np.random.default_rng(runs[0] * 7 + runs[1])
+    w = synth.make('small', seed=21, genome_bases=2_000_000, n_tx=900, iupac_rate=2e-3)
+    w.ex_len = rng.integers(1, 401, size=w.n_exons).astype(np.int64)
+    check_against_oracle(_recase(w, rng, *runs))
+
+
 def test_degenerate_intervals_vs_c_oracle():
     """Zero-length intervals, records shorter than one codon, 1-2 base
     exons mixed with long ones, and intervals clamped at contig ends."""
