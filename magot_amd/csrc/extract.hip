@@ -224,6 +224,19 @@ __device__ __forceinline__ void patch_runs(const Planes& a, uint64_t glo, uint64
   }
 }
 
+// Unified coordinate U of tile byte 0 for interval row {gw, o0, o1}: chunk
+// byte p of the tile reads unified base U + p (forward strand g = gs + (p -
+// s), reverse strand 2*span-1 - (gs + len-1 - (p - s)), s = o0 - T0).  U may
+// wrap below 0 for an interval that starts far into the tile; U + p does not,
+// and it is below 2^33 (genome < 4 Gbases), so 33 bits of U are enough.
+__device__ __forceinline__ uint64_t row_anchor(uint64_t gw, uint64_t o0, uint64_t o1, uint64_t T0,
+                                               uint64_t span) {
+  const uint64_t gs = gw & ~kExFlagBits;
+  const uint64_t s = o0 - T0;
+  return (gw & kRcBit) ? 2 * span - gs - (o1 - o0) - s : gs - s;
+}
+constexpr uint64_t kUMask = (1ull << 33) - 1;
+
 // General chunk assembly: any number of interval segments, exception runs.
 __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
                                                const uint4* ex) {
@@ -240,15 +253,15 @@ __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
     const int j0 = pos - p;
     const int n = min((int)X.z, end) - pos;
     const bool rc = (X.w & kFlagRc) != 0;
-    const uint64_t U = (uint64_t)X.x | ((uint64_t)X.y << 32);
+    const uint64_t U = (uint64_t)X.y | ((uint64_t)((X.w >> 12) & 1u) << 32);  // U mod 2^33
     uint32_t x0, x1;
-    window(a.nib, U + (uint64_t)p, x0, x1);  // chunk byte k <- unified base U + p + k
+    window(a.nib, (U + (uint64_t)p) & kUMask, x0, x1);  // chunk byte k <- unified base U + p + k
     const uint64_t m = (n >= 16 ? ~0ull : ((1ull << (4 * n)) - 1ull)) << (4 * j0);
     o.x0 = bfi((uint32_t)m, x0, o.x0);
     o.x1 = bfi((uint32_t)(m >> 32), x1, o.x1);
     if (X.w & kFlagExc) {
       // forward coordinates of chunk bytes j0 .. j0+n-1
-      const uint64_t u0 = U + (uint64_t)pos;
+      const uint64_t u0 = (U + (uint64_t)pos) & kUMask;
       const uint64_t glo = rc ? 2 * a.span - 1 - (u0 + (uint64_t)(n - 1)) : u0;
       patch_runs(a, glo, glo + (uint64_t)(n - 1), rc, j0, o);
     }
@@ -353,17 +366,19 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
     const int j = lane + 64 * h;
     if (j < m) {
       const uint64_t o0 = rows.o0[h], o1 = rows.o1[h], gw = rows.g[h];
-      const bool rc = (gw & kRcBit) != 0;
-      const uint64_t gs = gw & ~kExFlagBits;
       const int64_t s = (int64_t)(o0 - d.T0);
       const int64_t e = (int64_t)(o1 - d.T0);
-      // chunk byte p of the tile reads unified base U + p: forward g = gs + (p - s),
-      // reverse strand 2*span-1 - (gs + len-1 - (p - s))
-      const uint64_t U = rc ? 2 * span - gs - (o1 - o0) - (uint64_t)s : gs - (uint64_t)s;
+      const uint64_t U = row_anchor(gw, o0, o1, d.T0, span);
       const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
-      const uint32_t fl = (rc ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u) |
-                          ((gw & kSlowLitBit) ? kFlagSlowLit : 0u);
-      L.ex[j] = make_uint4((uint32_t)U, (uint32_t)(U >> 32), end32, fl);
+      const uint32_t fl = ((gw & kRcBit) ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u) |
+                          ((gw & kSlowLitBit) ? kFlagSlowLit : 0u) | ((uint32_t)(U & 7) << 8) |
+                          ((uint32_t)(U >> 32) & 1u) << 12;
+      // byte offset of the plane word holding tile byte 0's base (mod 2^32:
+      // U may wrap below 0, the chunks the row serves do not); chunk c reads
+      // its window at bN + 8c, funnel shift 4 * (U & 7).  The slow path takes
+      // U mod 2^33 from {y, flag bit 12}.
+      const uint32_t bN = (uint32_t)((int64_t)U >> 3) << 2;
+      L.ex[j] = make_uint4(bN, (uint32_t)U, end32, fl);
       if (j >= 1) {
         const int cj = ((int)s + kChunk - 1) / kChunk;
         if (cj < g.n_all) atomicAdd(&codes[cj], 1u);
@@ -409,8 +424,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* pla
                                            (int)0xFFFFFFFFu, 0x00020000);
 }
 
-__device__ __forceinline__ uint3 load_window(__amdgpu_buffer_rsrc_t plane, uint64_t u) {
-  const uint32_t off = __builtin_amdgcn_alignbit((uint32_t)(u >> 32), (uint32_t)u, 1) & ~3u;
+__device__ __forceinline__ uint3 load_window(__amdgpu_buffer_rsrc_t plane, uint32_t off) {
   const auto v = __builtin_amdgcn_raw_buffer_load_b96(plane, off, 0, MAGOT_EXP_LOAD_AUX);
   return make_uint3(v[0], v[1], v[2]);
 }
@@ -418,22 +432,29 @@ __device__ __forceinline__ uint3 load_window(__amdgpu_buffer_rsrc_t plane, uint6
 // Fast-path chunk assembly from prefetched windows: both segments read their
 // strand's half of the plane forward, so this is two funnel shifts per
 // segment and a masked merge at nibble n1.
-__device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, uint32_t& x0,
-                                           uint32_t& x1) {
+// Nibble masks of segment A by n1 (bytes from A, 1..16) for x0 and x1.
+__device__ __forceinline__ uint2 seg_masks(uint32_t n1) {
+  const uint32_t mlo = n1 >= 8 ? 0xFFFFFFFFu : ((1u << (4 * n1)) - 1u);
+  const uint32_t mhi = n1 >= 16 ? 0xFFFFFFFFu : (n1 <= 8 ? 0u : ((1u << (4 * (n1 - 8))) - 1u));
+  return make_uint2(mlo, mhi);
+}
+
+__device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, const uint2* masks,
+                                           uint32_t& x0, uint32_t& x1) {
   const uint32_t sa = (mt >> 6) & 28u, sb = (mt >> 14) & 28u;  // 4 * (u & 7)
   const uint32_t a0 = funnel(A.y, A.x, sa), a1 = funnel(A.z, A.y, sa);
   const uint32_t b0 = funnel(B.y, B.x, sb), b1 = funnel(B.z, B.y, sb);
-  // n1 = bytes from segment A (16 when the chunk is one segment)
-  const uint32_t n1 = (mt >> 24) & 31u;
-  const uint32_t mlo = n1 >= 8 ? 0xFFFFFFFFu : ((1u << (4 * n1)) - 1u);
-  const uint32_t mhi = n1 >= 16 ? 0xFFFFFFFFu : (n1 <= 8 ? 0u : ((1u << (4 * (n1 - 8))) - 1u));
-  x0 = bfi(mlo, a0, b0);
-  x1 = bfi(mhi, a1, b1);
+  // n1 = bytes from segment A (16 when the chunk is one segment): masks from
+  // the wave's LDS table (seg_masks)
+  const uint2 m = masks[(mt >> 24) & 31u];
+  x0 = bfi(m.x, a0, b0);
+  x1 = bfi(m.y, a1, b1);
 }
 
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   __shared__ WaveLds s_wave[kWaves];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[64];
+  __shared__ uint2 s_mask[17];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -461,10 +482,12 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   // arguments and then reads only what it wrote itself: no workgroup
   // barrier and no memory round trip before the tile's own loads.
   {
-    uint32_t v = 0;
+    // lane i takes word i of the table from the scalar argument (v_writelane)
+    int v = 0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v = lane == i ? a.lut[i] : v;
-    if (lane < 16) reinterpret_cast<uint32_t*>(s_lut)[lane] = v;
+    for (int i = 0; i < 16; ++i) asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(a.lut[i]), "i"(i));
+    if (lane < 16) reinterpret_cast<uint32_t*>(s_lut)[lane] = (uint32_t)v;
+    if (lane <= 16) s_mask[lane] = seg_masks((uint32_t)lane);  // identical in every wave
   }
   if (lane < kGuard) {
     L.codes_g[lane] = 0;
@@ -474,6 +497,11 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   const TileGeom g = geom(a, d);
   stage(L, codes, valid32, d, g, load_rows(a, d, lane), a.span, lane);
   const uint64_t T0 = d.T0;
+
+  // Chunks at tile bytes p < edge_lo or p >= edge_hi lie in the 128-byte lines
+  // the tile shares with its neighbours (plain stores there, store16_edge).
+  const int edge_lo = (int)((((T0 >> 7) + 1) << 7) - T0);
+  const int edge_hi = (int)((((d.T1 - 1) >> 7) << 7) - T0);
 
   // ---- nucleotide chunks: issue every window load first -------------------
   const __amdgpu_buffer_rsrc_t nib_rs = plane_rsrc(a.nib);
@@ -488,23 +516,21 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     const uint4 X = L.ex[i];
     const uint4 Y = L.ex[min(i + 1, (int)d.m - 1)];
     const int cend = min(p + kChunk, g.lim);
-    const uint64_t UA = (uint64_t)X.x | ((uint64_t)X.y << 32);
-    const uint64_t UB = (uint64_t)Y.x | ((uint64_t)Y.y << 32);
     const int n1 = min((int)X.z, cend) - p;  // bytes of segment A (1..16)
     const bool two = n1 < cend - p;
-    const uint64_t wa = UA + (uint64_t)p;
-    const uint64_t wb = two ? UB + (uint64_t)p : wa;
-    const bool slow = ((X.w | (two ? Y.w : 0u)) & kFlagSlowLit) != 0 || (two && (int)Y.z < cend) ||
+    const uint32_t fb = two ? Y.w : X.w;
+    const bool slow = ((X.w | fb) & kFlagSlowLit) != 0 || (two && (int)Y.z < cend) ||
                       (a.outputs & kDebugSlowNuc);
+    const uint32_t offa = X.x + 8u * (uint32_t)c;
+    const uint32_t offb = two ? Y.x + 8u * (uint32_t)c : offa;
     meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (slow ? 16u : 0u) |
-              ((uint32_t)(wa & 7) << 8) | ((uint32_t)(wb & 7) << 16) |
-              ((uint32_t)(two ? n1 : 16) << 24);
-    wA[k] = load_window(nib_rs, wa);
-    wB[k] = load_window(nib_rs, wb);
+              (X.w & 0x700u) | ((fb & 0x700u) << 8) | ((uint32_t)(two ? n1 : 16) << 24);
+    wA[k] = load_window(nib_rs, offa);
+    wB[k] = load_window(nib_rs, offb);
   }
   uint32_t x0k[kLaneChunks], x1k[kLaneChunks];
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) fast_chunk(wA[k], wB[k], meta[k], x0k[k], x1k[k]);
+  for (int k = 0; k < kLaneChunks; ++k) fast_chunk(wA[k], wB[k], meta[k], s_mask, x0k[k], x1k[k]);
   uint32_t slow_any = 0, exc_any = 0;
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) {
@@ -537,7 +563,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
       if (want_nuc && c < g.n_out)
         store16_edge(a.nuc + T0 + (uint64_t)p,
                      any_exc ? chunk_ascii_lit(x0k[k], x1k[k], ex, lit) : chunk_ascii(x0k[k], x1k[k], ex, lit),
-                     ((T0 + (uint64_t)p) >> 7) == (T0 >> 7) || ((T0 + (uint64_t)p) >> 7) == ((d.T1 - 1) >> 7));
+                     p < edge_lo || p >= edge_hi);
       if (want_pep) {
         codes[c] = pack_codes(x0k[k], x1k[k]);
         valid16[c] = (uint16_t)~(any_exc ? (ex | exc_bits(x0k[k], x1k[k])) : ex);
