@@ -463,6 +463,20 @@ class AnnotationSet(object):
         kwargs['annotation_set_to_modify'] = self
         read_gff(gff, *args, **kwargs)
 
+    def read_exonerate(self, exonerate_output):
+        """genome.py:569-570."""
+        read_exonerate(exonerate_output, annotation_set_to_modify=self)
+
+    def read_blast_csv(self, blast_csv, hierarchy=['match', 'match_part'], source='blast',
+                       find_truncated_locname=False):
+        """genome.py:572-573."""
+        read_blast_csv(blast_csv, annotation_set_to_modify=self, hierarchy=hierarchy,
+                       source=source, find_truncated_locname=find_truncated_locname)
+
+    def read_cegma_gff(self, cegma_gff):
+        """genome.py:575-576."""
+        read_cegma_gff(cegma_gff, annotation_set_to_modify=self)
+
     def get_fasta(self, feature, seq_type='nucleotide', longest=False, genomic=False, order=None):
         """genome.py:578-582, batched: one device launch for every record.
 
@@ -806,6 +820,173 @@ def read_gff(gff, annotation_set_to_modify=None, base_features=['CDS', 'match_pa
 
 
 # ---------------------------------------------------------------------------
+# Aligner outputs as match / match_part annotations (genome.py:32-121,
+# 418-499): the inputs of genome_tools blast_csv2fasta / exonerate2fasta,
+# which extract them through the same get_fasta path.
+# ---------------------------------------------------------------------------
+
+def vulgar2gff(vulgarlist, feature_types=['match', 'match_part'], source='exonerate'):
+    """genome.py:32-86: one exonerate vulgar record -> GFF lines (a match
+    line, then a match_part line per run of M/S/G/F operations).  Reference
+    quirks kept: the match_part bounds are min/max over the coordinate
+    STRINGS (lexicographic), and a '-' target keeps its start and moves its
+    end up by one."""
+    qname = vulgarlist[0] + '-against-' + vulgarlist[4]
+    tname = vulgarlist[4]
+    tstart = vulgarlist[5]
+    tend = vulgarlist[6]
+    tstrand = vulgarlist[7]
+    score = vulgarlist[8]
+    trips = vulgarlist[9:]
+    addfeat = False
+    idnum = 1
+    if tstrand == '+':
+        tpos = int(tstart) + 1
+    else:
+        tpos = int(tstart)
+        tend = str(int(tend) + 1)
+    lines = ['\t'.join([tname, source, feature_types[0], str(tpos), tend, score, tstrand, '.',
+                        'ID=' + qname])]
+    head = coords = None
+    for i in range(len(trips)):
+        field = trips[i]
+        if i % 3 == 0:
+            if field in ('M', 'S', 'G', 'F'):
+                if not addfeat:
+                    addfeat = True
+                    head = [tname, source, feature_types[1]]
+                    coords = [str(tpos)]
+            elif addfeat:
+                lines.append('\t'.join(head + [min(coords), max(coords), '.', tstrand, '.',
+                                               'ID=' + qname + '_' + feature_types[1] + str(idnum) +
+                                               ';Parent=' + qname]))
+                idnum += 1
+                addfeat = False
+        if i % 3 == 2:
+            if tstrand == '+':
+                tpos += int(field)
+            elif tstrand == '-':
+                tpos -= int(field)
+            if addfeat:
+                if tstrand == '+':
+                    coords.append(str(tpos - 1))
+                elif tstrand == '-':
+                    coords.append(str(tpos + 1))
+    if addfeat:
+        lines.append('\t'.join(head + [min(coords), max(coords), '.', tstrand, '.',
+                                       'ID=' + qname + '_' + feature_types[1] + str(idnum) +
+                                       ';Parent=' + qname]))
+    return '\n'.join(lines)
+
+
+def read_exonerate(exonerate_output, annotation_set_to_modify=None):
+    """genome.py:88-121: the Query / Target header lines name the next vulgar
+    record (':[revcomp]' / '[revcomp]' stripped from the target, one trailing
+    space dropped); a repeated query-target pair gets a numbered query name.
+    The GFF goes through read_gff into the set (no copy)."""
+    aset = AnnotationSet() if annotation_set_to_modify is None else annotation_set_to_modify
+    gfflines = []
+    seen = {}
+    qname = ''
+    tname = ''
+    for raw in ensure_file(exonerate_output):
+        line = raw.replace('\r', '').replace('\n', '')
+        if line[:16] == '         Query: ':
+            qname = line[16:]
+        elif line[:16] == '        Target: ':
+            tname = line[16:].replace(':[revcomp]', '').replace('[revcomp]', '')
+            if tname[-1] == ' ':
+                tname = tname[:-1]
+        elif line[:8] == 'vulgar: ':
+            vl = line[8:].split()
+            vl[0] = qname
+            vl[4] = tname
+            key = vl[0] + '-against-' + vl[4]
+            if key in seen:
+                vl[0] = vl[0] + str(seen[key])
+                seen[key] = seen[key] + 1
+            else:
+                seen[key] = 1
+            gfflines.append(vulgar2gff(vl))
+    read_gff('\n'.join(gfflines), annotation_set_to_modify=aset)
+    if annotation_set_to_modify is None:
+        return aset
+
+
+def read_cegma_gff(cegma_gff, annotation_set_to_modify=None):
+    """genome.py:418-422 (the CEGMA preset raises, see read_gff)."""
+    aset = read_gff(cegma_gff, annotation_set_to_modify=annotation_set_to_modify, presets='CEGMA')
+    if annotation_set_to_modify is None:
+        return aset
+
+
+def read_blast_csv(blast_csv, annotation_set_to_modify=None, hierarchy=['match', 'match_part'],
+                   source='blast', find_truncated_locname=False):
+    """genome.py:425-499: BLAST -outfmt 10 rows (more than 8 fields) ->
+    one base feature (hierarchy[-1]) per row under a chain of parents named
+    ID + '-' + parent type.  Subject coordinates give the strand (start <
+    end: '+', else '-').  A repeated query ID becomes ID-1, ID-2, ..."""
+    rows = ensure_file(blast_csv)
+    aset = AnnotationSet() if annotation_set_to_modify is None else annotation_set_to_modify
+    gen = {}
+    feature_type = hierarchy[-1]
+    chain = hierarchy[:-1]
+    chain.reverse()
+    if feature_type not in aset.__dict__:
+        setattr(aset, feature_type, {})
+    if find_truncated_locname:
+        if aset.genome is None:
+            _emit('"warning: find_truncated_locname" was set to true, but annotation set has no '
+                  'associated genome object so this cannot be done')
+            find_truncated_locname = False
+        else:
+            genome_seqids = aset.genome.get_seqids()
+    for raw in rows:
+        line = raw.replace('\r', '').replace('\n', '')
+        fields = line.split(',')
+        if len(fields) > 8:
+            seqid = fields[1]
+            if find_truncated_locname and seqid not in genome_seqids:
+                for full in genome_seqids:
+                    if seqid == full.split()[0]:
+                        seqid = full
+                        break
+            tstart = int(fields[8])
+            tend = int(fields[9])
+            if tstart < tend:
+                coords, strand = (tstart, tend), '+'
+            else:
+                coords, strand = (tend, tstart), '-'
+            score = fields[11]
+            base = fields[0]
+            table = getattr(aset, feature_type)
+            if base in table:
+                ID = base + '-' + str(gen[base])
+                gen[base] = gen[base] + 1
+                while ID in table:
+                    ID = base + '-' + str(gen[base])
+                    gen[base] = gen[base] + 1
+            else:
+                ID = base
+                gen[base] = 1
+            extra = {'evalue': fields[10], 'score': score}
+            parent = ID + '-' + chain[0]
+            child = ID
+            for level in range(len(chain)):
+                ptype = chain[level]
+                if ptype not in aset.__dict__:
+                    setattr(aset, ptype, {})
+                up = ID + '-' + chain[level + 1] if level != len(chain) - 1 else None
+                aset.__dict__[ptype][ID + '-' + ptype] = ParentAnnotation(
+                    ID + '-' + ptype, seqid, ptype, [child], up, strand, aset, other_attributes={})
+                child = ID + '-' + ptype
+            getattr(aset, feature_type)[ID] = BaseAnnotation(ID, seqid, coords, feature_type,
+                                                             parent, strand, extra, aset)
+    if annotation_set_to_modify is None:
+        return aset
+
+
+# ---------------------------------------------------------------------------
 # Genome facade (genome.py:880-978)
 # ---------------------------------------------------------------------------
 
@@ -828,9 +1009,15 @@ class Genome(object):
             elif annotation_format == 'gff3':
                 self.annotations = read_gff(annotations)
                 self.annotations.genome = self
-            elif annotation_format in ('cegma_gff', 'blast_csv', 'exonerate_output'):
-                raise NotImplementedError(annotation_format + ' readers are outside the '
-                                          'extraction path (SURVEY.md section 2, row 6)')
+            elif annotation_format == 'cegma_gff':
+                self.annotations = read_cegma_gff(annotations)
+                self.annotations.genome = self
+            elif annotation_format == 'blast_csv':
+                self.annotations = read_blast_csv(annotations)
+                self.annotations.genome = self
+            elif annotation_format == 'exonerate_output':
+                self.annotations = read_exonerate(annotations)
+                self.annotations.genome = self
         else:
             self.annotations = annotations
 
@@ -852,6 +1039,31 @@ class Genome(object):
             raise NotImplementedError('from_annotations is outside the extraction path')
         return ids
 
+    def read_exonerate(self, exonerate_output):
+        """genome.py:950-955."""
+        if self.annotations is not None:
+            self.annotations.read_exonerate(exonerate_output)
+        else:
+            self.annotations = read_exonerate(exonerate_output)
+            self.annotations.genome = self
+
+    def read_blast_csv(self, blast_csv, hierarchy=['match', 'match_part'], source='blast',
+                       find_truncated_locname=False):
+        """genome.py:957-961."""
+        if self.annotations is None:
+            self.annotations = AnnotationSet()
+            self.annotations.genome = self
+        self.annotations.read_blast_csv(blast_csv, hierarchy=hierarchy, source=source,
+                                        find_truncated_locname=find_truncated_locname)
+
+    def read_cegma_gff(self, cegma_gff):
+        """genome.py:963-968."""
+        if self.annotations is not None:
+            self.annotations.read_cegma_gff(cegma_gff)
+        else:
+            self.annotations = read_cegma_gff(cegma_gff)
+            self.annotations.genome = self
+
     def read_gff(self, gff, *args, **kwargs):
         """genome.py:970-975."""
         if self.annotations is not None:
@@ -862,4 +1074,5 @@ class Genome(object):
 
 
 __all__ = ['Genome', 'GenomeSequence', 'AnnotationSet', 'BaseAnnotation', 'ParentAnnotation',
-           'Sequence', 'read_gff', 'ensure_file', 'DEFAULT_ORDER']
+           'Sequence', 'read_gff', 'read_exonerate', 'read_blast_csv', 'read_cegma_gff',
+           'vulgar2gff', 'ensure_file', 'DEFAULT_ORDER']

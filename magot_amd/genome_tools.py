@@ -9,6 +9,9 @@
     python -m magot_amd.genome_tools coords2fasta <fasta> <seqid> <start> <stop> [truncate_names=False]
     python -m magot_amd.genome_tools dna2orfs <fasta> <output_file>   (broken in the reference:
            TypeError, reproduced)
+    python -m magot_amd.genome_tools blast_csv2fasta <fasta> <blast.csv> [order=py2|insertion]
+    python -m magot_amd.genome_tools exonerate2fasta <fasta> <exonerate.txt> [order=py2|insertion]
+    python -m magot_amd.genome_tools get_seq_from_fasta <fasta> <seq_name> [truncate_names=False]
 
 Arguments follow the reference's CLI convention (genome_tools.py:25-45):
 positional values, then ``key=value`` pairs, all strings.  The reference
@@ -227,6 +230,39 @@ def coords2fasta(fasta_file, seqid, start, stop, truncate_names='False'):
     _write(_gather(seqs, [(index[seqid], st, ln, False)])[0] + '\n')
 
 
+def _match_fasta(g, order):
+    """genome_tools.py:268-271 / 277-280: every match record's get_fasta(),
+    joined with newlines and printed; all records gathered in one launch
+    (AnnotationSet.get_fasta('match') is that same join).  The match dict is
+    built by insertion, never copied: Python-2 order after zero copies."""
+    if 'match' not in g.annotations.__dict__:
+        raise AttributeError("AnnotationSet instance has no attribute 'match'")
+    _write(g.annotations.get_fasta('match', order=order) + '\n')
+
+
+def blast_csv2fasta(genome_sequence, blast_csv, order='py2'):
+    """genome_tools.py:265-271: BLAST -outfmt 10 hits -> subject sequences
+    (reverse-complemented where the subject runs backwards)."""
+    g = genome.Genome(genome_sequence)
+    g.read_blast_csv(blast_csv)
+    _match_fasta(g, order)
+
+
+def exonerate2fasta(genome_sequence, exonerate_file, order='py2'):
+    """genome_tools.py:274-280: exonerate vulgar alignments -> the target
+    sequence of each alignment's aligned blocks, spliced."""
+    g = genome.Genome(genome_sequence)
+    g.read_exonerate(exonerate_file)
+    _match_fasta(g, order)
+
+
+def get_seq_from_fasta(genome_sequence, seq_name, truncate_names='False'):
+    """genome_tools.py:483-485: one contig as FASTA (host only: a whole
+    contig is a copy, not a gather)."""
+    g = genome.Genome(genome_sequence, truncate_names=_literal(truncate_names))
+    _write(g.get_scaffold_fasta(seq_name) + '\n')
+
+
 def dna2orfs(fasta_location, output_file, from_atg=False, longest=False):
     """genome_tools.py:145-180.  The reference builds a Genome, opens
     output_file for writing and then calls ``.translate(frame=, strand=)`` on
@@ -244,7 +280,9 @@ def dna2orfs(fasta_location, output_file, from_atg=False, longest=False):
 
 TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep,
          'extract_upstream_downstream': extract_upstream_downstream,
-         'coords2fasta': coords2fasta, 'dna2orfs': dna2orfs}
+         'coords2fasta': coords2fasta, 'dna2orfs': dna2orfs,
+         'blast_csv2fasta': blast_csv2fasta, 'exonerate2fasta': exonerate2fasta,
+         'get_seq_from_fasta': get_seq_from_fasta}
 
 
 def parse_argv(argv):

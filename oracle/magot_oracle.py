@@ -379,10 +379,12 @@ def _no_get_seq():
 
 def read_gff(src, base_features=('CDS', 'match_part', 'similarity', 'region'),
              features_to_ignore=('exon',), gff_version='auto', parents_hierarchy=(),
-             features_to_replace=(), IDfield='ID', parent_field='Parent', out=None):
+             features_to_replace=(), IDfield='ID', parent_field='Parent', out=None, into=None):
     """genome.py:242-415 (module read_gff), presets omitted (not on the path).
 
-    Returns an OracleSet, or None where the reference returns None.
+    Returns an OracleSet, or None where the reference returns None.  ``into``
+    is annotation_set_to_modify: that set is filled in place and returned
+    (no deep copy, genome.py:413-415).
     """
     base_features = list(base_features)
     features_to_ignore = list(features_to_ignore) if not isinstance(features_to_ignore, str) \
@@ -392,7 +394,7 @@ def read_gff(src, base_features=('CDS', 'match_part', 'similarity', 'region'),
     for pair in features_to_replace:
         repl['\t' + pair[0] + '\t'] = '\t' + pair[1] + '\t'
     version = gff_version
-    aset = OracleSet()
+    aset = OracleSet() if into is None else into
     renames = {}
     for raw in _lines(src):
         if raw[0] == '#' or raw.count('\t') != 8:
@@ -517,7 +519,7 @@ def read_gff(src, base_features=('CDS', 'match_part', 'similarity', 'region'),
             aset.__dict__[ftype][ID] = OBase(ID, seqid, coords, ftype, parent, strand, attrs, aset)
         else:
             aset.__dict__[ftype][ID] = OParent(ID, seqid, ftype, [], parent, strand, aset, attrs)
-    return copy.deepcopy(aset)
+    return copy.deepcopy(aset) if into is None else aset
 
 
 def load(fasta, gff, truncate_names=False, **kw):
@@ -685,3 +687,160 @@ def dna2orfs(fasta_file, from_atg=False, longest=False):
     for _ in seqs:
         return '', TypeError('translate() takes no keyword arguments')
     return '', None
+
+
+# ---------------------------------------------------------------------------
+# Aligner outputs (genome.py:32-121, 425-499) and their extraction tools
+# (genome_tools.py:265-280, 483-485)
+# ---------------------------------------------------------------------------
+
+def vulgar2gff(v, feature_types=('match', 'match_part'), source='exonerate'):
+    """genome.py:32-86.  v = vulgar fields: query, qstart, qend, qstrand,
+    target, tstart, tend, tstrand, score, then (op, query len, target len)
+    triplets.  The target cursor starts at tstart+1 ('+') or tstart ('-',
+    whose end also moves up by one); it advances by each target length, and
+    every run of M/S/G/F ops is one match_part whose bounds are the min and
+    max of its cursor positions compared as strings."""
+    qname = v[0] + '-against-' + v[4]
+    tname, tstart, tend, tstrand, score = v[4], v[5], v[6], v[7], v[8]
+    if tstrand == '+':
+        cur = int(tstart) + 1
+    else:
+        cur = int(tstart)
+        tend = str(int(tend) + 1)
+    out = [tname + '\t' + source + '\t' + feature_types[0] + '\t' + str(cur) + '\t' + tend +
+           '\t' + score + '\t' + tstrand + '\t.\tID=' + qname]
+    part = None      # cursor positions (strings) of the open match_part
+    n = 0
+
+    def close():
+        out.append('\t'.join([tname, source, feature_types[1], min(part), max(part), '.',
+                              tstrand, '.', 'ID=%s_%s%d;Parent=%s' % (qname, feature_types[1],
+                                                                     n + 1, qname)]))
+
+    trips = v[9:]
+    for i, f in enumerate(trips):
+        if i % 3 == 0:
+            if f in ('M', 'S', 'G', 'F'):
+                if part is None:
+                    part = [str(cur)]
+            elif part is not None:
+                close()
+                n += 1
+                part = None
+        elif i % 3 == 2:
+            step = int(f)
+            if tstrand == '+':
+                cur += step
+                if part is not None:
+                    part.append(str(cur - 1))
+            elif tstrand == '-':
+                cur -= step
+                if part is not None:
+                    part.append(str(cur + 1))
+    if part is not None:
+        close()
+    return '\n'.join(out)
+
+
+def read_exonerate(src, into=None):
+    """genome.py:88-121."""
+    aset = OracleSet() if into is None else into
+    q = t = ''
+    seen = {}
+    gff = []
+    for raw in _lines(src):
+        line = raw.replace('\r', '').replace('\n', '')
+        if line.startswith('         Query: '):
+            q = line[16:]
+        elif line.startswith('        Target: '):
+            t = line[16:].replace(':[revcomp]', '').replace('[revcomp]', '')
+            if t[-1] == ' ':
+                t = t[:-1]
+        elif line.startswith('vulgar: '):
+            v = line[8:].split()
+            v[0], v[4] = q, t
+            k = q + '-against-' + t
+            if k in seen:
+                v[0] = q + str(seen[k])
+                seen[k] += 1
+            else:
+                seen[k] = 1
+            gff.append(vulgar2gff(v))
+    read_gff('\n'.join(gff), into=aset)
+    return aset
+
+
+def read_blast_csv(src, into=None, hierarchy=('match', 'match_part'), source='blast',
+                   find_truncated_locname=False, out=None):
+    """genome.py:425-499 (fields: 0 query, 1 subject, 8/9 subject start/end,
+    10 evalue, 11 score)."""
+    aset = OracleSet() if into is None else into
+    base = hierarchy[-1]
+    parents = list(hierarchy[:-1])[::-1]
+    if base not in aset.__dict__:
+        aset.__dict__[base] = {}
+    names = None
+    if find_truncated_locname:
+        if aset.genome is None:
+            _say(out, '"warning: find_truncated_locname" was set to true, but annotation set '
+                      'has no associated genome object so this cannot be done')
+        else:
+            names = list(aset.genome.genome_sequence)
+    counters = {}
+    for raw in _lines(src):
+        f = raw.replace('\r', '').replace('\n', '').split(',')
+        if len(f) <= 8:
+            continue
+        sid = f[1]
+        if names is not None and sid not in names:
+            sid = next((n for n in names if n.split()[0] == sid), sid)
+        a, b = int(f[8]), int(f[9])
+        coords, strand = ((a, b), '+') if a < b else ((b, a), '-')
+        score, qid = f[11], f[0]
+        tbl = aset.__dict__[base]
+        if qid in tbl:
+            while True:
+                ID = qid + '-' + str(counters[qid])
+                counters[qid] += 1
+                if ID not in tbl:
+                    break
+        else:
+            ID = qid
+            counters[qid] = 1
+        attrs = {'evalue': f[10], 'score': score}
+        child = ID
+        for i, pt in enumerate(parents):
+            up = ID + '-' + parents[i + 1] if i < len(parents) - 1 else None
+            aset.__dict__.setdefault(pt, {})[ID + '-' + pt] = OParent(
+                ID + '-' + pt, sid, pt, [child], up, strand, aset, {})
+            child = ID + '-' + pt
+        tbl[ID] = OBase(ID, sid, coords, base, ID + '-' + parents[0], strand, attrs, aset)
+    return aset
+
+
+def _match_tool(aset, order, out=None):
+    d = getattr(aset, 'match')  # AttributeError without any match (the reference's loop)
+    keys = py2_dict_order(list(d)) if order == 'py2' else list(d)
+    return '\n'.join(get_fasta(d[k], aset, out=out) for k in keys) + '\n'
+
+
+def blast_csv2fasta(fasta, blast_csv, order='insertion', out=None):
+    """genome_tools.py:265-271 -> stdout text (record order: the match dict's,
+    insertion or Python 2 after zero copies)."""
+    aset = OracleSet(OracleGenome(read_fasta(fasta)))
+    read_blast_csv(blast_csv, into=aset, out=out)
+    return _match_tool(aset, order, out)
+
+
+def exonerate2fasta(fasta, exonerate_output, order='insertion', out=None):
+    """genome_tools.py:274-280 -> stdout text."""
+    aset = OracleSet(OracleGenome(read_fasta(fasta)))
+    read_exonerate(exonerate_output, into=aset)
+    return _match_tool(aset, order, out)
+
+
+def get_seq_from_fasta(fasta, seq_name, truncate_names='False'):
+    """genome_tools.py:483-485 -> stdout text."""
+    seqs = read_fasta(fasta, truncate_names=truncate_names == 'True')
+    return '>' + seq_name + '\n' + seqs[seq_name] + '\n'

@@ -16,6 +16,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   synth_small.json hashes of gff2fasta on the seeded small synthetic
   loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
   orfs.json       dna2orfs output files (six-frame ORFs of whole contigs)
+  matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -347,8 +348,151 @@ def make_orfs(ref):
     return out
 
 
+def _match_genome():
+    """Three contigs (one header with a description), soft-masked runs, N runs
+    and IUPAC bytes; chrA is long enough for target coordinates to cross 999
+    -> 1000 (vulgar2gff compares coordinate strings)."""
+    rnd = random.Random(265)
+    out = []
+    for name, n in (('chrA', 1500), ('chrB desc text', 800), ('chrC', 300)):
+        s = [rnd.choice('ACGT') for _ in range(n)]
+        for _ in range(n // 120):
+            a = rnd.randrange(n)
+            for k in range(a, min(n, a + rnd.randrange(5, 60))):
+                s[k] = s[k].lower()
+        a = rnd.randrange(n - 20)
+        for k in range(a, a + 7):
+            s[k] = 'N'
+        s[rnd.randrange(n)] = rnd.choice('RYKM')
+        seq = ''.join(s)
+        out.append('>' + name + '\n' + '\n'.join(seq[i:i + 70] for i in range(0, n, 70)) + '\n')
+    return ''.join(out)
+
+
+BLAST_CSV = '\n'.join([
+    'q1,chrA,98.0,100,2,0,1,100,101,200,1e-40,180',
+    'q2,chrA,97.5,80,2,0,1,80,400,321,1e-30,150',       # subject runs backwards: '-'
+    'q1,chrC,90.0,50,5,0,1,50,10,59,1e-10,60',          # repeated query: q1-1
+    'q1,chrA,90.0,50,5,0,1,50,1200,1151,1e-10,61',      # q1-2, '-'
+    'q3,chrA,99.0,30,0,0,1,30,995,1024,1e-12,55',
+    'q4,chrA,99.0,1,0,0,1,1,700,700,1,2',               # start == end: '-'
+    'q5,chrB desc text,95.0,60,3,0,1,60,30,89,1e-20,100',
+    'q6,chrC,95.0,60,3,0,1,60,270,330,1e-20,100',       # runs past the contig end
+    'short,row,only',                                   # <= 8 fields: skipped
+    'q7,chrA,91.0,40,4,0,1,40,1,40,1e-8,70',
+]) + '\n'
+
+BLAST_TRUNC = 'q8,chrB,95.0,60,3,0,1,60,100,159,1e-20,100\nq9,chrA,95.0,20,3,0,1,20,5,24,1,9\n'
+
+EXONERATE = """Command line: [exonerate --model protein2genome p.fa g.fa]
+Hostname: [box]
+
+C4 Alignment:
+------------
+         Query: prot1 first protein
+        Target: chrA
+         Model: protein2genome:local
+   Raw score: 240
+vulgar: prot1 0 60 . chrA 100 330 + 240 M 30 90 5 0 2 I 0 40 3 0 2 M 20 60 F 0 1 M 10 30 G 0 3
+C4 Alignment:
+------------
+         Query: prot2
+        Target: chrA:[revcomp]
+vulgar: prot2 0 40 . chrA 1050 900 - 150 M 20 60 5 0 2 I 0 20 3 0 2 S 1 2 M 19 57 N 0 3 G 2 0
+C4 Alignment:
+------------
+         Query: prot2
+        Target: chrA:[revcomp]
+vulgar: prot2 5 30 . chrA 1300 1220 - 90 M 25 75 3 0 2
+C4 Alignment:
+------------
+         Query: prot3 crossing
+        Target: chrA 
+vulgar: prot3 0 12 . chrA 980 1016 + 60 M 5 15 I 0 6 M 5 15
+C4 Alignment:
+------------
+         Query: prot4
+        Target: chrB desc text [revcomp]
+vulgar: prot4 0 20 . chrB 300 240 - 50 M 20 60
+-- completed exonerate analysis
+"""
+
+
+def make_matches(ref):
+    """genome_tools blast_csv2fasta (:265-271), exonerate2fasta (:274-280) and
+    get_seq_from_fasta (:483-485) of the reference, stdout captured; plus
+    the library readers (read_blast_csv with find_truncated_locname, the
+    Genome constructor's blast_csv / exonerate_output formats) and the
+    Python-2 record order (the match dict after zero copies)."""
+    sys.path.insert(0, PY3)
+    import genome_tools as rt
+    import tempfile
+    fa_text = _match_genome()
+    out = {'_inputs': {'genome': fa_text, 'blast_csv': BLAST_CSV, 'blast_trunc': BLAST_TRUNC,
+                       'exonerate': EXONERATE}}
+    with tempfile.TemporaryDirectory() as td:
+        paths = {}
+        for k, text in (('fa', fa_text), ('csv', BLAST_CSV), ('trunc', BLAST_TRUNC),
+                        ('ex', EXONERATE), ('csv_bad', 'q1,chrA,1,1,1,1,1,1,x,20,1,1\n'),
+                        ('csv_missing', 'q1,chrZ,1,1,1,1,1,1,10,20,1,1\n'),
+                        ('csv_empty', 'no,rows\n'),
+                        # a query named like a generated ID: KeyError in the reference
+                        ('csv_clash', BLAST_CSV + 'q1-1,chrA,88.0,20,2,0,1,20,50,69,1e-3,30\n')):
+            paths[k] = os.path.join(td, k)
+            with open(paths[k], 'w') as fh:
+                fh.write(text)
+        for tag, fn, args in (
+                ('blast', rt.blast_csv2fasta, (paths['fa'], paths['csv'])),
+                ('blast_trunc_tool', rt.blast_csv2fasta, (paths['fa'], paths['trunc'])),
+                ('blast_bad_int', rt.blast_csv2fasta, (paths['fa'], paths['csv_bad'])),
+                ('blast_missing_seqid', rt.blast_csv2fasta, (paths['fa'], paths['csv_missing'])),
+                ('blast_no_rows', rt.blast_csv2fasta, (paths['fa'], paths['csv_empty'])),
+                ('blast_clash', rt.blast_csv2fasta, (paths['fa'], paths['csv_clash'])),
+                ('exonerate', rt.exonerate2fasta, (paths['fa'], paths['ex'])),
+                ('seq/chrA', rt.get_seq_from_fasta, (paths['fa'], 'chrA')),
+                ('seq/chrB desc text', rt.get_seq_from_fasta, (paths['fa'], 'chrB desc text')),
+                ('seq/chrB truncated', rt.get_seq_from_fasta, (paths['fa'], 'chrB', 'True')),
+                ('seq/missing', rt.get_seq_from_fasta, (paths['fa'], 'chrQ'))):
+            res, exc, so = call(lambda: fn(*args))
+            out['tool/' + tag] = {'exc': exc, 'stdout': so}
+
+        def lib(build):
+            def run():
+                g = build()
+                d = g.annotations.match
+                keys = list(d)
+                res = {}
+                for order, ks in (('insertion', keys), ('py2', mo.py2_dict_order(keys))):
+                    res[order] = '\n'.join(d[k].get_fasta() for k in ks)
+                prot = []
+                for k in keys:  # per record: a record shorter than a codon raises
+                    r, e, _ = call(lambda: d[k].get_fasta(seq_type='protein'))
+                    prot.append({'exc': e} if e else r)
+                res['protein'] = prot
+                res['ids'] = sorted(g.annotations.match_part)
+                return res
+            return run
+
+        def g_trunc():
+            g = ref.Genome(paths['fa'])
+            g.read_blast_csv(paths['trunc'], find_truncated_locname=True)
+            return g
+
+        for tag, build in (
+                ('blast_ctor', lambda: ref.Genome(paths['fa'], paths['csv'],
+                                                  annotation_format='blast_csv')),
+                ('exonerate_ctor', lambda: ref.Genome(paths['fa'], paths['ex'],
+                                                      annotation_format='exonerate_output')),
+                ('blast_truncated_locname', g_trunc)):
+            res, exc, so = call(lib(build))
+            out['lib/' + tag] = {'exc': exc, 'stdout': so, 'result': res}
+    return out
+
+
 def main():
     ref = reference_module()
+    with open(os.path.join(HERE, 'matches.json'), 'w') as fh:
+        json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:
         json.dump(make_locus(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'orfs.json'), 'w') as fh:

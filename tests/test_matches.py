@@ -1,0 +1,234 @@
+"""Aligner outputs on the extraction path: genome_tools.blast_csv2fasta
+(genome_tools.py:265-271), exonerate2fasta (:274-280) and get_seq_from_fasta
+(:483-485), with the readers they use -- read_blast_csv (genome.py:425-499),
+read_exonerate and vulgar2gff (genome.py:32-121).
+
+tests/golden/matches.json holds the REFERENCE's own stdout / exception for
+every case (tests/golden/make_golden.py).  CPU: the oracle restatement
+reproduces them, and the drop-in readers build the same annotation graph as
+the oracle (no GPU needed for parsing).  GPU (marked): the drop-in tools,
+which gather every match record with one extraction-kernel launch, reproduce
+the reference's bytes, in both record orders.
+"""
+import contextlib
+import io
+import json
+import os
+import random
+
+import pytest
+
+import goldlib
+from oracle import magot_oracle as mo
+
+GOLD = json.load(open(os.path.join(goldlib.HERE, 'matches.json')))
+INP = GOLD['_inputs']
+
+# tool cases: golden key -> (input file key, tool, extra args)
+TOOL_CASES = {
+    'tool/blast': ('csv', 'blast_csv2fasta', ()),
+    'tool/blast_trunc_tool': ('trunc', 'blast_csv2fasta', ()),
+    'tool/blast_bad_int': ('csv_bad', 'blast_csv2fasta', ()),
+    'tool/blast_missing_seqid': ('csv_missing', 'blast_csv2fasta', ()),
+    'tool/blast_no_rows': ('csv_empty', 'blast_csv2fasta', ()),
+    'tool/blast_clash': ('csv_clash', 'blast_csv2fasta', ()),
+    'tool/exonerate': ('ex', 'exonerate2fasta', ()),
+}
+
+
+@pytest.fixture(scope='module')
+def files(tmp_path_factory):
+    d = tmp_path_factory.mktemp('matches')
+    texts = {'fa': INP['genome'], 'csv': INP['blast_csv'], 'trunc': INP['blast_trunc'],
+             'ex': INP['exonerate'], 'csv_bad': 'q1,chrA,1,1,1,1,1,1,x,20,1,1\n',
+             'csv_missing': 'q1,chrZ,1,1,1,1,1,1,10,20,1,1\n', 'csv_empty': 'no,rows\n',
+             'csv_clash': INP['blast_csv'] + 'q1-1,chrA,88.0,20,2,0,1,20,50,69,1e-3,30\n'}
+    paths = {}
+    for k, t in texts.items():
+        paths[k] = str(d / k)
+        with open(paths[k], 'w') as fh:
+            fh.write(t)
+    return paths
+
+
+def _capture(fn, *args):
+    buf = io.BytesIO()
+    out = io.TextIOWrapper(buf, encoding='latin-1', write_through=True)
+    exc = None
+    res = None
+    with contextlib.redirect_stdout(out):
+        try:
+            res = fn(*args)
+        except Exception as e:  # noqa: BLE001
+            exc = type(e).__name__
+    out.flush()
+    return buf.getvalue().decode('latin-1'), exc, res
+
+
+# ---------------------------------------------------------------------------
+# CPU: the oracle against the reference's outputs
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize('key', sorted(TOOL_CASES))
+def test_oracle_tools_match_reference(files, key):
+    src, tool, _ = TOOL_CASES[key]
+    fn = {'blast_csv2fasta': mo.blast_csv2fasta, 'exonerate2fasta': mo.exonerate2fasta}[tool]
+    prints, exc, text = _capture(fn, files['fa'], files[src])
+    want = GOLD[key]
+    assert exc == want['exc']
+    if exc is None:
+        assert prints + text == want['stdout']
+    else:
+        assert prints == want['stdout']
+
+
+@pytest.mark.parametrize('key', [k for k in GOLD if k.startswith('tool/seq/')])
+def test_oracle_get_seq_from_fasta(files, key):
+    name = {'chrA': 'chrA', 'chrB desc text': 'chrB desc text', 'chrB truncated': 'chrB',
+            'missing': 'chrQ'}[key[len('tool/seq/'):]]
+    trunc = 'True' if key.endswith('truncated') else 'False'
+    _, exc, text = _capture(mo.get_seq_from_fasta, files['fa'], name, trunc)
+    assert exc == GOLD[key]['exc']
+    if exc is None:
+        assert text == GOLD[key]['stdout']
+
+
+def _oracle_lib(files, tag):
+    aset = mo.OracleSet(mo.OracleGenome(mo.read_fasta(files['fa'])))
+    if tag == 'blast_ctor':
+        mo.read_blast_csv(files['csv'], into=aset)
+    elif tag == 'exonerate_ctor':
+        mo.read_exonerate(files['ex'], into=aset)
+    else:
+        mo.read_blast_csv(files['trunc'], into=aset, find_truncated_locname=True)
+    return aset
+
+
+@pytest.mark.parametrize('tag', ['blast_ctor', 'exonerate_ctor', 'blast_truncated_locname'])
+def test_oracle_readers_match_reference(files, tag):
+    want = GOLD['lib/' + tag]['result']
+    aset = _oracle_lib(files, tag)
+    d = aset.__dict__['match']
+    assert sorted(aset.__dict__['match_part']) == want['ids']
+    for order, keys in (('insertion', list(d)), ('py2', mo.py2_dict_order(list(d)))):
+        assert '\n'.join(mo.get_fasta(d[k], aset) for k in keys) == want[order]
+    for k, w in zip(list(d), want['protein']):
+        try:
+            got = mo.get_fasta(d[k], aset, seq_type='protein')
+        except TypeError:
+            got = {'exc': 'TypeError'}
+        assert got == w
+
+
+# ---------------------------------------------------------------------------
+# CPU: the drop-in readers build the oracle's annotation graph
+# ---------------------------------------------------------------------------
+
+def _random_vulgar(rnd, strand):
+    ops = []
+    for _ in range(rnd.randrange(1, 9)):
+        op = rnd.choice('MMMSGFI53N')
+        ops += [op, str(rnd.randrange(0, 40)), str(rnd.randrange(0, 130))]
+    t0 = rnd.randrange(900, 1100)
+    t1 = t0 + 200 if strand == '+' else t0 - 200
+    return ['q%d' % rnd.randrange(5), '0', '50', '.', 'chrA', str(t0), str(t1), strand,
+            str(rnd.randrange(1000))] + ops
+
+
+def test_vulgar2gff_matches_oracle():
+    from magot_amd import genome as G
+    rnd = random.Random(7)
+    for i in range(400):
+        v = _random_vulgar(rnd, '+-.'[i % 3])
+        assert G.vulgar2gff(list(v)) == mo.vulgar2gff(list(v)), v
+
+
+def _graph(d):
+    """Comparable view of an annotation set: per feature table, per ID."""
+    out = {}
+    for name, tbl in d.items():
+        if type(tbl) is not dict:
+            continue
+        out[name] = {k: ('Parent' if hasattr(o, 'child_list') else 'Base', o.seqid,
+                         getattr(o, 'coords', None), o.strand, list(getattr(o, 'child_list', [])),
+                         o.parent)
+                     for k, o in tbl.items()}
+    return out
+
+
+@pytest.mark.parametrize('which', ['blast', 'exonerate'])
+def test_readers_match_oracle_graph(files, which):
+    from magot_amd import genome as G
+    if which == 'blast':
+        mine = G.read_blast_csv(files['csv'])
+        ref = mo.read_blast_csv(files['csv'])
+    else:
+        mine = G.read_exonerate(files['ex'])
+        ref = mo.read_exonerate(files['ex'])
+    assert _graph(mine.__dict__) == _graph(ref.__dict__)
+
+
+def test_blast_reader_errors_match_reference(files):
+    from magot_amd import genome as G
+    for src, want in (('csv_bad', 'ValueError'), ('csv_clash', 'KeyError')):
+        with pytest.raises(Exception) as e:
+            G.read_blast_csv(files[src])
+        assert type(e.value).__name__ == want
+
+
+# ---------------------------------------------------------------------------
+# GPU: the drop-in tools (one extraction launch per tool call)
+# ---------------------------------------------------------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('key', sorted(TOOL_CASES))
+def test_gpu_tools_match_reference(files, key):
+    from magot_amd import genome_tools
+    src, tool, _ = TOOL_CASES[key]
+    text, exc, _ = _capture(getattr(genome_tools, tool), files['fa'], files[src], 'insertion')
+    assert exc == GOLD[key]['exc']
+    assert text == GOLD[key]['stdout']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('tag', ['blast_ctor', 'exonerate_ctor', 'blast_truncated_locname'])
+def test_gpu_readers_and_orders_match_reference(files, tag):
+    from magot_amd import genome as G
+    want = GOLD['lib/' + tag]['result']
+    if tag == 'blast_ctor':
+        g = G.Genome(files['fa'], files['csv'], annotation_format='blast_csv')
+    elif tag == 'exonerate_ctor':
+        g = G.Genome(files['fa'], files['ex'], annotation_format='exonerate_output')
+    else:
+        g = G.Genome(files['fa'])
+        g.read_blast_csv(files['trunc'], find_truncated_locname=True)
+    assert sorted(g.annotations.match_part) == want['ids']
+    for order in ('insertion', 'py2'):
+        assert g.annotations.get_fasta('match', order=order) == want[order]
+    for k, w in zip(list(g.annotations.match), want['protein']):
+        try:
+            got = g.annotations.match[k].get_fasta(seq_type='protein')
+        except TypeError:
+            got = {'exc': 'TypeError'}
+        assert got == w
+
+
+@pytest.mark.gpu
+def test_gpu_tool_py2_order(files):
+    from magot_amd import genome_tools
+    for tool, src, tag in (('blast_csv2fasta', 'csv', 'blast_ctor'),
+                           ('exonerate2fasta', 'ex', 'exonerate_ctor')):
+        text, exc, _ = _capture(getattr(genome_tools, tool), files['fa'], files[src])  # py2
+        assert exc is None
+        assert text == GOLD['lib/' + tag]['result']['py2'] + '\n'
+
+
+@pytest.mark.parametrize('key', [k for k in GOLD if k.startswith('tool/seq/')])
+def test_get_seq_from_fasta_tool(files, key):
+    from magot_amd import genome_tools
+    name = {'chrA': 'chrA', 'chrB desc text': 'chrB desc text', 'chrB truncated': 'chrB',
+            'missing': 'chrQ'}[key[len('tool/seq/'):]]
+    trunc = 'True' if key.endswith('truncated') else 'False'
+    text, exc, _ = _capture(genome_tools.get_seq_from_fasta, files['fa'], name, trunc)
+    assert exc == GOLD[key]['exc']
+    assert text == GOLD[key]['stdout']
