@@ -99,15 +99,18 @@ void magot_ctx_destroy(magot_ctx* ctx);
  * exception bit per base) plus its reverse-complement mirror, and a run list
  * of every byte that is not ACGTacgt (N, IUPAC, '-', spaces ...) with a
  * 4096-base directory.  seqs[i] points at lens[i] raw bytes of contig i,
- * exactly the bytes genome.py:875 keeps (every byte except CR/LF).  Genomes
- * up to 4 Gbases per device (MAGOT_ERR_ARG above).
+ * exactly the bytes genome.py:875 keeps (every byte except CR/LF).  One
+ * device plane holds up to ~4 Gbases; above that MAGOT_ERR_UNSUPPORTED, and
+ * the caller packs the contigs as several planes, one magot_genome each
+ * (magot_amd.engine.PartitionedGenome: one plan per plane).
  * Replaces: GenomeSequence (genome.py:854-877) as the data the path reads.
  */
 int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
                       uint32_t n_contigs, magot_genome** out);
 /*
  * Read FASTA text (GenomeSequence, genome.py:854-877, incl. truncate_names)
- * natively and pack it like magot_genome_load.  MAGOT_ERR_UNSUPPORTED for
+ * natively and pack it like magot_genome_load (MAGOT_ERR_UNSUPPORTED above
+ * one device plane, as there).  MAGOT_ERR_UNSUPPORTED also for
  * headers whose whitespace split differs between the reference's Python 2
  * byte strings and Python 3 (bytes >= 0x80, 0x1c-0x1f) or that are empty
  * under truncate_names: the caller then uses the Python reader.

@@ -242,6 +242,17 @@ int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, mag
     fprintf(stderr, "[genome] %-8s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
     t0 = t1;
   };
+  {
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < n_contigs; ++i) total += src[i].len;
+    // the packed span (kOrigin + bases + padding, pack_genome) must stay below
+    // 4 Gi nibble bytes: 32-bit window offsets in extract_kernel
+    if (total + kOrigin + 256 > 0xFFFFFFF0ull) {
+      set_error("magot_genome_load: genomes above 4 Gbases take several device planes "
+                "(engine.PartitionedGenome)");
+      return MAGOT_ERR_UNSUPPORTED;
+    }
+  }
   HostPacked hp;
   pack_genome(src, n_contigs, &hp);
   lap("pack");
@@ -250,8 +261,8 @@ int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, mag
     return MAGOT_ERR_ARG;
   }
   if (2 * hp.nib_words * 4 + 16 > 0xFFFFFFFFull) {  // 32-bit buffer offsets (extract.hip)
-    set_error("magot_genome_load: genomes above 4 Gbases are not supported");
-    return MAGOT_ERR_ARG;
+    set_error("magot_genome_load: genomes above 4 Gbases take several device planes");
+    return MAGOT_ERR_UNSUPPORTED;
   }
   std::unique_ptr<magot_genome> g(new magot_genome());
   g->ctx = ctx;

@@ -3,6 +3,7 @@ raw-sequence batch ops.  Everything here runs on the GPU through libmagot.so;
 there is no host compute path."""
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -116,6 +117,144 @@ class DeviceGenome(object):
             self.close()
         except Exception:
             pass
+
+
+# One device plane addresses < 4 Gbases (32-bit window offsets, extract.hip);
+# a larger genome is packed as several planes (PartitionedGenome).
+PART_BASES = int(os.environ.get('MAGOT_GENOME_PART_BASES', '3500000000'))
+
+
+def plan_parts(lengths, limit=None):
+    """Contigs (in order) -> part index per contig: consecutive contigs share
+    a part while its bases stay <= limit.  A contig above the limit cannot be
+    packed (MagotError)."""
+    limit = PART_BASES if limit is None else limit
+    part = np.zeros(len(lengths), dtype=np.int64)
+    k, acc = 0, 0
+    for i, n in enumerate(int(x) for x in lengths):
+        if n > limit:
+            raise MagotError('contig %d has %d bases: above the %d-base device plane' %
+                             (i, n, limit))
+        if acc and acc + n > limit:
+            k, acc = k + 1, 0
+        part[i] = k
+        acc += n
+    return part
+
+
+class PartitionedGenome(object):
+    """A genome above one device plane: contigs cut into parts (plan_parts),
+    each packed into its own HBM arena.  Extraction over it runs one plan per
+    part (extract_records)."""
+
+    def __init__(self, contigs, ctx=None, limit=None):
+        contigs = list(contigs)
+        self.ctx = ctx or _lib.default_context()
+        self.names = [n for n, _ in contigs]
+        self.index = {nm: i for i, nm in enumerate(self.names)}
+        self.lengths = np.array([len(s) for _, s in contigs], dtype=np.uint64)
+        self.part_of = plan_parts(self.lengths, limit)
+        n_parts = int(self.part_of.max()) + 1 if len(contigs) else 0
+        self.local = np.zeros(len(contigs), dtype=np.int64)
+        self.parts = []
+        for k in range(n_parts):
+            idx = np.nonzero(self.part_of == k)[0]
+            self.local[idx] = np.arange(len(idx))
+            self.parts.append(DeviceGenome([contigs[i] for i in idx], ctx=self.ctx))
+        self.total_bases = int(self.lengths.sum())
+
+    def close(self):
+        for g in self.parts:
+            g.close()
+        self.parts = []
+
+
+def device_genome(contigs, ctx=None):
+    """DeviceGenome, or PartitionedGenome above PART_BASES bases."""
+    contigs = list(contigs)
+    if sum(len(s) for _, s in contigs) > PART_BASES:
+        return PartitionedGenome(contigs, ctx=ctx)
+    return DeviceGenome(contigs, ctx=ctx)
+
+
+def extract_records(genome, exons, txs, outputs=OUT_NUC | OUT_PEP):
+    """ExtractionPlan(genome, exons, txs, outputs).run() over either genome
+    kind.  On a PartitionedGenome: one plan (one launch) per part; a record
+    whose intervals lie in two parts is gathered as one-interval pieces in
+    their parts, joined, and translated in one translate_batch launch."""
+    if not isinstance(genome, PartitionedGenome):
+        plan = ExtractionPlan(genome, exons, txs, outputs)
+        try:
+            return plan.run()
+        finally:
+            plan.close()
+    exons = np.ascontiguousarray(exons, dtype=EXON_DTYPE)
+    txs = np.ascontiguousarray(txs, dtype=TX_DTYPE)
+    T = len(txs)
+    begin = txs['exon_begin'].astype(np.int64)
+    count = txs['n_exons'].astype(np.int64)
+    ex_part = genome.part_of[exons['contig'].astype(np.int64)] if len(exons) else \
+        np.zeros(0, np.int64)
+    rec_part = np.zeros(T, dtype=np.int64)
+    cross = np.zeros(T, dtype=bool)
+    for t in np.nonzero(count > 0)[0]:
+        ps = ex_part[begin[t]:begin[t] + count[t]]
+        rec_part[t] = ps[0]
+        cross[t] = bool((ps != ps[0]).any())
+    rec_len = np.zeros(T, dtype=np.int64)
+    if len(exons):
+        cs = np.concatenate([[0], np.cumsum(exons['len'].astype(np.int64))])
+        rec_len = cs[begin + count] - cs[begin]
+    noff = np.zeros(T + 1, dtype=np.uint64)
+    np.cumsum(rec_len, out=noff[1:])
+    want_pep = bool(outputs & OUT_PEP)
+    pep_len = rec_len // 3
+    poff = np.zeros(T + 1, dtype=np.uint64)
+    np.cumsum(pep_len, out=poff[1:])
+    nuc = np.empty(int(noff[-1]), dtype=np.uint8) if outputs & OUT_NUC or cross.any() else None
+    pep = np.empty(int(poff[-1]), dtype=np.uint8) if want_pep else None
+    for k, part in enumerate(genome.parts):
+        whole = np.nonzero((rec_part == k) & ~cross)[0]
+        pieces = [e for t in np.nonzero(cross)[0]
+                  for e in range(begin[t], begin[t] + count[t]) if ex_part[e] == k]
+        if len(whole) == 0 and not pieces:
+            continue
+        sub_ex = [exons[begin[t]:begin[t] + count[t]] for t in whole] + \
+            [exons[e:e + 1] for e in pieces]
+        sub_ex = np.concatenate(sub_ex) if sub_ex else np.zeros(0, EXON_DTYPE)
+        sub_ex['contig'] = genome.local[sub_ex['contig'].astype(np.int64)]
+        cnt = np.concatenate([count[whole], np.ones(len(pieces), np.int64)])
+        sub_tx = np.zeros(len(cnt), dtype=TX_DTYPE)
+        sub_tx['n_exons'] = cnt
+        sub_tx['exon_begin'] = np.cumsum(cnt) - cnt
+        sub_out = outputs | (OUT_NUC if pieces else 0)
+        n_k, no_k, p_k, po_k = extract_records(part, sub_ex, sub_tx, sub_out)
+        for i, t in enumerate(whole):
+            if nuc is not None and n_k is not None:
+                nuc[int(noff[t]):int(noff[t + 1])] = n_k[int(no_k[i]):int(no_k[i + 1])]
+            if want_pep:
+                pep[int(poff[t]):int(poff[t + 1])] = p_k[int(po_k[i]):int(po_k[i + 1])]
+        piece_bytes = {}
+        for j, e in enumerate(pieces):
+            i = len(whole) + j
+            piece_bytes[e] = n_k[int(no_k[i]):int(no_k[i + 1])]
+        for t in np.nonzero(cross)[0]:
+            o = int(noff[t])
+            for e in range(begin[t], begin[t] + count[t]):
+                ln = int(exons['len'][e])
+                if e in piece_bytes:
+                    nuc[o:o + ln] = piece_bytes[e]
+                o += ln
+    if want_pep and cross.any():
+        ids = np.nonzero(cross)[0]
+        seqs = [nuc[int(noff[t]):int(noff[t + 1])].tobytes().decode('latin-1') for t in ids]
+        peps = translate_batch(seqs, [0] * len(seqs), ['+'] * len(seqs))
+        for t, pstr in zip(ids, peps):
+            pep[int(poff[t]):int(poff[t + 1])] = np.frombuffer(
+                (pstr or '').encode('latin-1'), dtype=np.uint8)
+    if not outputs & OUT_NUC:
+        nuc = None
+    return nuc, noff, pep, poff
 
 
 def fasta_read(text, truncate_names=False):
@@ -501,4 +640,4 @@ def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
 
 __all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'OUT_NUC',
            'OUT_PEP', 'MagotError', 'GffPlan', 'orf6_batch', 'Orf6Plan', 'fasta_read',
-           'FastaGenome']
+           'FastaGenome', 'PartitionedGenome', 'device_genome', 'extract_records', 'plan_parts']

@@ -271,14 +271,14 @@ class GenomeSequence(dict):
     def device(self):
         """The engine.DeviceGenome of this dict (packed once, cached)."""
         if self._device is None:
-            self._device = engine.DeviceGenome(list(self.items()))
+            self._device = engine.device_genome(list(self.items()))
         return self._device
 
 
 def _device_genome_for(seqdict):
     if isinstance(seqdict, GenomeSequence):
         return seqdict.device()
-    return engine.DeviceGenome(list(seqdict.items()))
+    return engine.device_genome(list(seqdict.items()))
 
 
 # ---------------------------------------------------------------------------
@@ -376,11 +376,7 @@ class _Batch(object):
             outputs |= engine.OUT_NUC
         if 'pep' in self.kinds:
             outputs |= engine.OUT_PEP
-        plan = engine.ExtractionPlan(self.genome, ex, tx, outputs)
-        try:
-            nuc, noff, pep, poff = plan.run()
-        finally:
-            plan.close()
+        nuc, noff, pep, poff = engine.extract_records(self.genome, ex, tx, outputs)
         nraw = nuc.tobytes().decode('latin-1') if nuc is not None else ''
         praw = pep.tobytes().decode('latin-1') if pep is not None else ''
         noff = noff.tolist()

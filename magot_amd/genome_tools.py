@@ -95,6 +95,8 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order):
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)
         dev = seqs.device()
+        if isinstance(dev, engine.PartitionedGenome):
+            return None  # several device planes: the object path extracts per plane
     names = dev.names
     protein = seq_type == 'protein'
     plan = engine.GffPlan.build(genome.read_buffer(gff), names, [int(x) for x in dev.lengths],
@@ -167,11 +169,7 @@ def _gather(seqs, intervals):
     tx = np.zeros(len(intervals), dtype=engine.TX_DTYPE)
     tx['exon_begin'] = np.arange(len(intervals))
     tx['n_exons'] = 1
-    plan = engine.ExtractionPlan(seqs.device(), ex, tx, engine.OUT_NUC)
-    try:
-        nuc, noff, _, _ = plan.run()
-    finally:
-        plan.close()
+    nuc, noff, _, _ = engine.extract_records(seqs.device(), ex, tx, engine.OUT_NUC)
     raw = nuc.tobytes().decode('latin-1')
     return [raw[int(noff[i]):int(noff[i + 1])] for i in range(len(intervals))]
 
