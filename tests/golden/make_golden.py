@@ -17,6 +17,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
   orfs.json       dna2orfs output files (six-frame ORFs of whole contigs)
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
+  fuzz.json       random small GFF3/GTF cases through gff2fasta's path
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -489,8 +490,101 @@ def make_matches(ref):
     return out
 
 
+def _fuzz_case(rnd):
+    """A small random genome + GFF3 or GTF that walks many of read_gff's and
+    get_fasta's branches: renamed duplicate IDs, reversed / zero / past-end
+    coordinates, '.', '-' and mixed strands, duplicate coordinates, UTR and
+    exon children, comment and short lines, shared parents."""
+    alpha = 'ACGTACGTACGTacgtNRY'
+    contigs = []
+    for i in range(rnd.randrange(1, 4)):
+        n = rnd.randrange(30, 260)
+        contigs.append(('s%d' % i if rnd.random() < 0.8 else 's%d desc' % i,
+                        ''.join(rnd.choice(alpha) for _ in range(n))))
+    fasta = ''.join('>%s\n%s\n' % (nm, sq) for nm, sq in contigs)
+    seqids = [nm for nm, _ in contigs]
+    lens = {nm: len(sq) for nm, sq in contigs}
+
+    def coords(sid):
+        a = rnd.randrange(0, lens[sid] + 3)
+        b = a + rnd.randrange(0, 60)
+        if rnd.random() < 0.15:
+            a, b = b, a
+        return a, b
+
+    lines = []
+    gtf = rnd.random() < 0.3
+    if gtf:
+        for g in range(rnd.randrange(1, 6)):
+            sid = rnd.choice(seqids)
+            st = rnd.choice('++--.')
+            for t in range(rnd.randrange(1, 3)):
+                for _ in range(rnd.randrange(1, 5)):
+                    a, b = coords(sid)
+                    lines.append('%s\tsrc\tCDS\t%d\t%d\t.\t%s\t0\ttranscript_id "g%d.t%d"; '
+                                 'gene_id "g%d";\n' % (sid, a, b, st, g, t, g))
+    else:
+        cds_ids = ['c%d' % k for k in range(4)]
+        for g in range(rnd.randrange(1, 6)):
+            sid = rnd.choice(seqids)
+            st = rnd.choice('++--.')
+            lines.append('%s\tsrc\tgene\t1\t%d\t.\t%s\t.\tID=g%d\n' % (sid, lens[sid], st, g))
+            for t in range(rnd.randrange(1, 3)):
+                tid = 'g%d.t%d' % (g, t)
+                lines.append('%s\tsrc\tmRNA\t1\t%d\t.\t%s\t.\tID=%s;Parent=g%d\n'
+                             % (sid, lens[sid], st, tid, g))
+                kids = []
+                for _ in range(rnd.randrange(1, 5)):
+                    a, b = coords(sid)
+                    if kids and rnd.random() < 0.1:
+                        a, b = kids[-1]
+                    kids.append((a, b))
+                    cst = st if rnd.random() < 0.85 else rnd.choice('+-')
+                    cid = rnd.choice(cds_ids) if rnd.random() < 0.5 else 'cds%d' % len(lines)
+                    lines.append('%s\tsrc\tCDS\t%d\t%d\t.\t%s\t%d\tID=%s;Parent=%s\n'
+                                 % (sid, a, b, cst, rnd.randrange(3), cid, tid))
+                if rnd.random() < 0.15:
+                    lines.append('%s\tsrc\texon\t1\t9\t.\t%s\t.\tID=e%d;Parent=%s\n'
+                                 % (sid, st, len(lines), tid))
+                if rnd.random() < 0.08:
+                    lines.append('%s\tsrc\tfive_prime_UTR\t1\t4\t.\t%s\t.\tID=u%d;Parent=%s\n'
+                                 % (sid, st, len(lines), tid))
+        if rnd.random() < 0.3:
+            lines.insert(rnd.randrange(len(lines) + 1), '# a comment\tline\n')
+        if rnd.random() < 0.2:
+            lines.insert(rnd.randrange(len(lines) + 1), 'short\tline\n')
+    return fasta, ''.join(lines)
+
+
+FUZZ_CALLS = [('nucleotide', False, 'insertion'), ('protein', False, 'insertion'),
+              ('nucleotide', True, 'insertion'), ('nucleotide', False, 'py2'),
+              ('protein', False, 'py2')]
+
+
+def make_fuzz(ref, n=60):
+    """Random small annotation sets through the reference's gff2fasta path
+    (Genome + read_gff + get_fasta, tests/test_fuzz.py)."""
+    rnd = random.Random(20261016)
+    out = []
+    for i in range(n):
+        fasta, gff = _fuzz_case(rnd)
+        rec = {'fasta': fasta, 'gff': gff, 'calls': {}}
+        for seq_type, longest, order in FUZZ_CALLS:
+            res, exc, so = ref_gff2fasta(ref, fasta, gff, seq_type, longest=longest, order=order)
+            d = {'exc': exc, 'stdout': so}
+            if res is not None:
+                d['sha256'] = sha(res)
+                if len(res) < 600:
+                    d['text'] = res
+            rec['calls']['%s/%d/%s' % (seq_type, int(longest), order)] = d
+        out.append(rec)
+    return out
+
+
 def main():
     ref = reference_module()
+    with open(os.path.join(HERE, 'fuzz.json'), 'w') as fh:
+        json.dump(make_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'matches.json'), 'w') as fh:
         json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:
