@@ -276,7 +276,18 @@ def dna2orfs(fasta_location, output_file, from_atg=False, longest=False):
             raise TypeError('translate() takes no keyword arguments')
 
 
-TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep,
+def get_CDS_peptides(genome_sequence, gff, output_location, gene_name_filters=[],
+                     gene_length_filter=None, names_from='CDS'):
+    """genome_tools.py:283-322.  The reference reads the genome, then calls
+    ``Genome.read_gff3``, which genome.py never defines: AttributeError
+    before the output file is opened (Python 2.7 and 3 alike).  Reproduced
+    as is; its intent, the longest ORF per CDS, is Sequence.get_orfs
+    (orf6_kernel) on each CDS's get_seq()."""
+    genome.Genome(genome_sequence)
+    raise AttributeError("Genome instance has no attribute 'read_gff3'")
+
+
+TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep, 'get_CDS_peptides': get_CDS_peptides,
          'extract_upstream_downstream': extract_upstream_downstream,
          'coords2fasta': coords2fasta, 'dna2orfs': dna2orfs,
          'blast_csv2fasta': blast_csv2fasta, 'exonerate2fasta': exonerate2fasta,

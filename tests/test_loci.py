@@ -136,3 +136,16 @@ def test_dna2orfs_matches_reference_failure(tmp_path):
     empty.write_text('')
     genome_tools.dna2orfs(str(empty), str(tmp_path / 'o2.txt'))  # no contig: no error
     assert (tmp_path / 'o2.txt').read_text() == ''
+
+
+def test_get_cds_peptides_matches_reference_failure(tmp_path):
+    """genome_tools.py:283-322 calls the undefined Genome.read_gff3: the
+    reference raises AttributeError after reading the genome and before it
+    opens the output file; so does the drop-in (no output file)."""
+    from magot_amd import genome_tools
+    fa = tmp_path / 'g.fa'
+    fa.write_text('>c1\nATGAAATAG\n')
+    dst = tmp_path / 'out.fa'
+    with pytest.raises(AttributeError):
+        genome_tools.get_CDS_peptides(str(fa), 'unused.gff', str(dst))
+    assert not dst.exists()
