@@ -81,14 +81,20 @@ void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out);
 constexpr int kThreads = 256;                 // one workgroup = 4 independent waves
 constexpr int kWaves = kThreads / 64;
 constexpr int kChunk = 16;                    // bytes per lane-store
-constexpr int kLaneChunks = 5;                // chunk slots per lane per tile
+#ifndef MAGOT_EXP_LANE_CHUNKS
+#define MAGOT_EXP_LANE_CHUNKS 5
+#endif
+constexpr int kLaneChunks = MAGOT_EXP_LANE_CHUNKS;  // chunk slots per lane per tile
 constexpr int kSlots = 64 * kLaneChunks;      // 320 chunk slots per wave tile
 constexpr int kTile = (kSlots - 3) * kChunk;  // 5072 output bytes per tile (3 slots of halo):
                                               // <= 1691 residues, <= 106 residue chunks
 constexpr int kPepPerLane = 2;                // residue chunk slots per lane
 constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
                                               // the residues rounded up to a 16-byte store
-constexpr int kExonCap = 128;                 // intervals staged in LDS per tile (7 blocks of 4 waves fit a CU's LDS)
+#ifndef MAGOT_EXP_EXON_CAP
+#define MAGOT_EXP_EXON_CAP 128
+#endif
+constexpr int kExonCap = MAGOT_EXP_EXON_CAP;  // intervals staged in LDS per tile (7 blocks of 4 waves fit a CU's LDS)
 constexpr int kTxCap = 64;                    // records staged in LDS per tile
 constexpr int kPepSlots = 64 * kPepPerLane;  // residue chunks per tile
 constexpr uint64_t kExcBit = 1ull << 62;      // interval touches an exception run
@@ -155,6 +161,21 @@ struct ExtractArgs {
   uint32_t outputs;
   uint32_t lut[16];           // 64 residue bytes indexed c0 + 4*c1 + 16*c2
 };
+
+// Dynamic LDS (never touched by the kernel) that caps a kernel at `want`
+// resident blocks per CU; 0 when it already fits or want <= 0.
+inline size_t occupancy_lds_pad(const void* fn, int threads, int want) {
+  if (want <= 0) return 0;
+  int dev = 0, lds_cu = 0, n = 0;
+  hipFuncAttributes at{};
+  if (hipGetDevice(&dev) != hipSuccess || hipFuncGetAttributes(&at, fn) != hipSuccess ||
+      hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) !=
+          hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, threads, 0) != hipSuccess || n <= want)
+    return 0;
+  const size_t need = (size_t)lds_cu / (size_t)(want + 1) + 1;  // > 1/(want+1) of the CU's LDS
+  return need > at.sharedSizeBytes ? need - at.sharedSizeBytes : 0;
+}
 
 void launch_extract(const ExtractArgs& a, hipStream_t s);
 int extract_blocks_per_cu();

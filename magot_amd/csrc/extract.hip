@@ -704,15 +704,34 @@ void launch_mirror_planes(uint32_t* nib, uint64_t span, hipStream_t s) {
                      nib, nw);
 }
 
+// Blocks of extract_kernel per CU.  Its registers and LDS allow 7 (70 VGPRs,
+// 22.4 KB per block); 6 runs faster: fewer tiles in flight contend less in the
+// memory system it is bound by.  A/B on one box, 3 alternating runs of the
+// default bench: 0.2729 / 0.2730 / 0.2728 ms per step at 6 blocks against
+// 0.2761 / 0.2761 / 0.2763 at 7 (5 blocks: 0.2749 / 0.2754 / 0.2762).  The cap
+// is dynamic LDS that the kernel never touches; MAGOT_EXTRACT_BLOCKS_PER_CU
+// overrides it (0: no cap).
+constexpr int kExtractBlocksPerCu = 6;
+
+size_t extract_lds_pad() {
+  static const size_t pad = [] {
+    const char* env = getenv("MAGOT_EXTRACT_BLOCKS_PER_CU");
+    const int want = env ? atoi(env) : kExtractBlocksPerCu;
+    return occupancy_lds_pad(reinterpret_cast<const void*>(extract_kernel), kThreads, want);
+  }();
+  return pad;
+}
+
 void launch_extract(const ExtractArgs& a, hipStream_t s) {
   if (a.n_tiles == 0) return;
   const uint32_t grid = (a.n_tiles + kWaves - 1) / kWaves;  // one tile per wave
-  hipLaunchKernelGGL(extract_kernel, dim3(grid), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(extract_kernel, dim3(grid), dim3(kThreads), extract_lds_pad(), s, a);
 }
 
 int extract_blocks_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extract_kernel, kThreads, 0) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extract_kernel, kThreads,
+                                                   extract_lds_pad()) != hipSuccess)
     return 0;
   return n;
 }
