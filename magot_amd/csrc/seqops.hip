@@ -770,9 +770,18 @@ void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_s
 void launch_orf6(const Orf6Args& a, bool genome, hipStream_t s) {
   if (a.n_tiles == 0) return;
   const uint64_t blocks = (a.n_tiles + kOpsThreads / 64 - 1) / (kOpsThreads / 64);
-  if (genome)
-    hipLaunchKernelGGL(orf6_kernel<true>, dim3((uint32_t)blocks), dim3(kOpsThreads), 0, s, a);
-  else
+  if (genome) {
+    // Occupancy knob for A/B (MAGOT_ORF6_BLOCKS_PER_CU; default no cap: 6
+    // blocks per CU, LDS-limited).  Unlike extract_kernel this kernel wants
+    // every wave it can get: caps of 5 / 4 blocks ran 6 % / 19 % slower, and a
+    // 7-block build (row cap 95, 32-word chunk bitmap) was no faster.
+    static const size_t pad = [] {
+      const char* env = getenv("MAGOT_ORF6_BLOCKS_PER_CU");
+      return occupancy_lds_pad(reinterpret_cast<const void*>(orf6_kernel<true>), kOpsThreads,
+                               env ? atoi(env) : 0);
+    }();
+    hipLaunchKernelGGL(orf6_kernel<true>, dim3((uint32_t)blocks), dim3(kOpsThreads), pad, s, a);
+  } else
     hipLaunchKernelGGL(orf6_kernel<false>, dim3((uint32_t)blocks), dim3(kOpsThreads), 0, s, a);
 }
 
