@@ -162,6 +162,18 @@ struct ExtractArgs {
   uint32_t lut[16];           // 64 residue bytes indexed c0 + 4*c1 + 16*c2
 };
 
+// Wave-wide inclusive prefix sum with DPP row shifts and row broadcasts
+// (gfx9 wave64: row_shr:1/2/4/8 inside rows of 16, then row_bcast:15/31).
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+  return v;
+}
+
 // Dynamic LDS (never touched by the kernel) that caps a kernel at `want`
 // resident blocks per CU; 0 when it already fits or want <= 0.
 inline size_t occupancy_lds_pad(const void* fn, int threads, int want) {

@@ -270,18 +270,6 @@ __device__ __noinline__ Chunk build_chunk_slow(Planes a, int p, int lim, int i,
   return o;
 }
 
-// Wave-wide inclusive prefix sum with DPP row shifts and row broadcasts
-// (gfx9 wave64: row_shr:1/2/4/8 inside rows of 16, then row_bcast:15/31).
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
-  return v;
-}
-
 struct TileDesc {
   uint64_t T0, T1, Q0, Q1;
   uint32_t eb, m, tb, nt;

@@ -171,6 +171,10 @@ constexpr int kOrfVecs = 256;        // staged 16-byte vectors per wave
 constexpr int kOrfBatch = 10;        // records per segment batch: one (record, stream) per lane
 constexpr int kOrfSegs = 6 * kOrfBatch;
 constexpr int kOrfRankWords = 128;   // chunk bitmap: a batch owns < 4096 chunks
+// A batch's chunks start inside the tile: per stream of a record at most
+// ov/48 + 1, ov = the record's overlap with the tile (sum over the batch <=
+// kOrfTile), six streams per record; far below the 16-bit scan field.
+static_assert(6 * (kOrfTile / 48 + 1 + kOrfBatch) < 32 * kOrfRankWords, "chunk bitmap too small");
 
 // real codons of frame f in a record of L bases (0 when translate() is None)
 __device__ __host__ __forceinline__ uint64_t orf_count(uint64_t L, uint32_t f) {
@@ -404,12 +408,7 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     {
       const uint4 c = s_stage[wave][lane];  // vectors 4 lane .. 4 lane + 3
       const uint32_t c0 = c.x, c1 = c0 + c.y, c2 = c1 + c.z, c3 = c2 + c.w;
-      uint32_t x = c3;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-      }
+      const uint32_t x = wave_scan(c3);
       const uint32_t base = x - c3 - 1;
       s_stage[wave][lane] = make_uint4(base + c0, base + c1, base + c2, base + c3);
     }
@@ -592,20 +591,16 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
       lo = min(lo, hi);
     }
     const uint32_t cnt = (uint32_t)(hi - lo);
-    // wave-inclusive scans: chunk starts and compacted segment slots
-    uint32_t incl = cnt, incl_s = cnt != 0;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d, 64), z = __shfl_up(incl_s, d, 64);
-      if (lane >= d) {
-        incl += y;
-        incl_s += z;
-      }
-    }
-    const uint32_t n_chunks = __shfl(incl, 63, 64);
-    const uint32_t n_minus = __shfl(incl, kOrfSegs / 2 - 1, 64);  // '-' chunks come first
+    // wave-inclusive scans of chunk starts (low half: a batch owns < 1024
+    // chunks, see kOrfRankWords) and compacted segment slots (high half), one
+    // DPP scan for both
+    const uint32_t sc = wave_scan(cnt | (cnt != 0 ? 1u << 16 : 0u));
+    const uint32_t incl = sc & 0xFFFFu, incl_s = sc >> 16;
+    const uint32_t n_chunks = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    // '-' chunks come first
+    const uint32_t n_minus = (uint32_t)__builtin_amdgcn_readlane((int)incl, kOrfSegs / 2 - 1);
     // does the next batch still start inside the tile?
-    const bool more = __shfl((int)(rec && nb + L < T1), kOrfSegs - 1, 64) &&
+    const bool more = __builtin_amdgcn_readlane((int)(rec && nb + L < T1), kOrfSegs - 1) != 0 &&
                       rb + kOrfBatch < a.n_rec;
     bm[lane] = 0u;
     bm[lane + 64] = 0u;
@@ -655,12 +650,7 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     __builtin_amdgcn_wave_barrier();
     {  // pre[w] = segment starts in words before w
       const uint32_t x0 = __popc(bm[2 * lane]), x1 = __popc(bm[2 * lane + 1]);
-      uint32_t x = x0 + x1;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-      }
+      const uint32_t x = wave_scan(x0 + x1);
       pre[2 * lane] = x - x0 - x1;
       pre[2 * lane + 1] = x - x1;
     }
