@@ -591,9 +591,12 @@ def py2_order_after_deepcopy(keys):
 
 
 def gff2fasta(fasta, gff, seq_type='nucleotide', longest=False, genomic=False, order='insertion',
-              out=None):
-    """genome_tools.py:324-330 (without from_exons): the text ``print`` writes."""
-    aset = load(fasta, gff, out=out)
+              out=None, from_exons=False):
+    """genome_tools.py:324-330: the text ``print`` writes.  from_exons reads
+    with features_to_ignore="CDS" (a string: substring test, as :327 passes
+    it) and exon -> CDS replaced."""
+    kw = {'features_to_ignore': 'CDS', 'features_to_replace': [('exon', 'CDS')]} if from_exons else {}
+    aset = load(fasta, gff, out=out, **kw)
     keys = None
     if order == 'py2':
         keys = py2_order_after_deepcopy(list(aset.gene))

@@ -190,10 +190,13 @@ def make_edges(ref):
 # ---------------------------------------------------------------------------
 
 def ref_gff2fasta(ref, fasta, gff, seq_type='nucleotide', longest=False, genomic=False,
-                  order='insertion'):
+                  order='insertion', from_exons=False):
     def run():
         g = ref.Genome(fasta)
-        g.read_gff(gff)
+        if from_exons:  # genome_tools.py:327
+            g.read_gff(gff, features_to_ignore="CDS", features_to_replace=[('exon', 'CDS')])
+        else:
+            g.read_gff(gff)
         if order == 'py2':
             keys = mo.py2_order_after_deepcopy(list(g.annotations.gene))
             g.annotations.gene = {k: g.annotations.gene[k] for k in keys}
@@ -581,10 +584,68 @@ def make_fuzz(ref, n=60):
     return out
 
 
+def _fuzz_case2(rnd):
+    """As _fuzz_case, with exon children beside the CDS (random coordinates,
+    strands and IDs) so that from_exons=True has exon structures to read."""
+    fasta, gff = _fuzz_case(rnd)
+    seqs = {}
+    for block in fasta.split('>')[1:]:
+        name, sq = block.split('\n', 1)
+        seqs[name] = len(sq.replace('\n', ''))
+    lines = []
+    for line in gff.splitlines(True):
+        lines.append(line)
+        f = line.split('\t')
+        if len(f) == 9 and f[2] == 'CDS' and rnd.random() < 0.7:
+            n = seqs.get(f[0], 100)
+            for _ in range(rnd.randrange(1, 3)):
+                a = rnd.randrange(0, n + 3)
+                b = a + rnd.randrange(0, 80)
+                if rnd.random() < 0.1:
+                    a, b = b, a
+                st = f[6] if rnd.random() < 0.9 else rnd.choice('+-')
+                if 'Parent=' in f[8]:
+                    par = f[8].split('Parent=')[1].split(';')[0].strip()
+                    attr = 'ID=%s;Parent=%s\n' % (rnd.choice(['ex%d' % len(lines), 'e1', 'e2']), par)
+                else:
+                    attr = f[8]
+                lines.append('\t'.join(f[:2] + ['exon', str(a), str(b), '.', st, '.', attr]))
+    return fasta, ''.join(lines)
+
+
+FUZZ2_CALLS = [('nucleotide', False, True, False, 'insertion'), ('protein', False, True, False, 'insertion'),
+               ('protein', True, False, False, 'insertion'), ('nucleotide', False, False, True, 'insertion'),
+               ('protein', False, False, True, 'insertion'), ('nucleotide', False, False, True, 'py2'),
+               ('nucleotide', True, False, True, 'insertion')]
+
+
+def make_fuzz2(ref, n=40):
+    """The gff2fasta options fuzz.json leaves out -- genomic=True, longest
+    protein, from_exons=True (exon features read as CDS) -- on random cases
+    with exon children (tests/test_fuzz.py)."""
+    rnd = random.Random(20261017)
+    out = []
+    for i in range(n):
+        fasta, gff = _fuzz_case2(rnd)
+        rec = {'fasta': fasta, 'gff': gff, 'calls': {}}
+        for seq_type, longest, genomic, from_exons, order in FUZZ2_CALLS:
+            res, exc, so = ref_gff2fasta(ref, fasta, gff, seq_type, longest=longest, genomic=genomic,
+                                         order=order, from_exons=from_exons)
+            d = {'exc': exc, 'stdout': so}
+            if res is not None:
+                d['sha256'] = sha(res)
+            rec['calls']['%s/%d/%d/%d/%s' % (seq_type, int(longest), int(genomic), int(from_exons),
+                                             order)] = d
+        out.append(rec)
+    return out
+
+
 def main():
     ref = reference_module()
     with open(os.path.join(HERE, 'fuzz.json'), 'w') as fh:
         json.dump(make_fuzz(ref), fh, indent=0, sort_keys=True)
+    with open(os.path.join(HERE, 'fuzz2.json'), 'w') as fh:
+        json.dump(make_fuzz2(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'matches.json'), 'w') as fh:
         json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:

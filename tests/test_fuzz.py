@@ -1,4 +1,5 @@
-"""Randomised gff2fasta cases against the REFERENCE (tests/golden/fuzz.json,
+"""Randomised gff2fasta cases against the REFERENCE (tests/golden/fuzz.json and
+fuzz2.json,
 made by tests/golden/make_golden.py from the reference's own Genome /
 read_gff / get_fasta): small genomes with lower case, N and IUPAC bytes, and
 GFF3 / GTF files with renamed duplicate IDs, reversed, zero and past-end
@@ -22,6 +23,8 @@ import goldlib
 from oracle import magot_oracle as mo
 
 CASES = json.load(open(os.path.join(goldlib.HERE, 'fuzz.json')))
+# genomic=True, longest protein and from_exons=True (exon features as CDS)
+CASES2 = json.load(open(os.path.join(goldlib.HERE, 'fuzz2.json')))
 
 
 def _sha(s):
@@ -81,4 +84,37 @@ def test_gpu_gff2fasta_matches_reference(i, native):
         seq_type, longest, order = call.split('/')
         full, exc = _run(genome_tools.gff2fasta, rec['fasta'], rec['gff'], seq_type=seq_type,
                          longest=str(longest == '1'), order=order, native=native)
+        _check(full, exc, want)
+
+
+def _call2(key):
+    seq_type, longest, genomic, from_exons, order = key.split('/')
+    return seq_type, longest == '1', genomic == '1', from_exons == '1', order
+
+
+@pytest.mark.parametrize('i', range(len(CASES2)))
+def test_oracle_options_match_reference(i):
+    rec = CASES2[i]
+    for call, want in sorted(rec['calls'].items()):
+        seq_type, longest, genomic, from_exons, order = _call2(call)
+
+        def run():
+            sys_out = mo.gff2fasta(rec['fasta'], rec['gff'], seq_type=seq_type, longest=longest,
+                                   genomic=genomic, order=order, from_exons=from_exons)
+            import sys
+            sys.stdout.write(sys_out)
+        full, exc = _run(run)
+        _check(full, exc, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('i', range(len(CASES2)))
+def test_gpu_gff2fasta_options_match_reference(i):
+    from magot_amd import genome_tools
+    rec = CASES2[i]
+    for call, want in sorted(rec['calls'].items()):
+        seq_type, longest, genomic, from_exons, order = _call2(call)
+        full, exc = _run(genome_tools.gff2fasta, rec['fasta'], rec['gff'],
+                         from_exons=str(from_exons), seq_type=seq_type, longest=str(longest),
+                         genomic=str(genomic), order=order)
         _check(full, exc, want)
