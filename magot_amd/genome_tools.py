@@ -121,6 +121,9 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order):
 def cds2pep(fasta_file):
     """genome_tools.py:664-675: headers echoed, each record translated; all
     records go to the GPU as one batch."""
+    if not hasattr(fasta_file, 'read'):
+        with open(fasta_file, 'rb'):  # the reference open()s the path (:666): a missing file raises
+            pass
     events = []       # ('line', text) | ('pep', job index)
     seqs = []
     failure = None

@@ -604,21 +604,25 @@ def gff2fasta(fasta, gff, seq_type='nucleotide', longest=False, genomic=False, o
                           order=keys, out=out) + '\n'
 
 
-def cds2pep(fasta):
-    """genome_tools.py:664-675: header lines echoed, each record translated."""
+def cds2pep(fasta, out=None):
+    """genome_tools.py:664-675: header lines echoed, each record translated.
+    With ``out`` (a text stream) every line is written as the reference
+    prints it, so a blank line's IndexError (:668, ``line[0]``) leaves the
+    lines before it; without, the text is returned."""
     outl = []
+    sink = (lambda t: out.write(t + '\n')) if out is not None else outl.append
     work = ''
     for raw in _lines(fasta):
         line = raw.replace('\n', '').replace('\r', '')
         if line[0] == '>':
             if work != '':
-                outl.append(str(translate(work)))
+                sink(str(translate(work)))
                 work = ''
-            outl.append(line)
+            sink(line)
         else:
             work = work + line
-    outl.append(str(translate(work)))
-    return '\n'.join(outl) + '\n'
+    sink(str(translate(work)))
+    return '\n'.join(outl) + '\n' if out is None else None
 
 
 # ---------------------------------------------------------------------------

@@ -640,12 +640,59 @@ def make_fuzz2(ref, n=40):
     return out
 
 
+def _cds_case(rnd):
+    """Random CDS FASTA text for cds2pep: headers with spaces, records of 0 to
+    90 bases (upper / lower case, N, IUPAC, '*'), sequence before the first
+    header, CRLF lines, no final newline, and (rarely) a blank line, which the
+    reference's line[0] turns into an IndexError.  ASCII only, no lone CR:
+    the reference is run as its Python 3 copy, whose text-mode open() would
+    split a lone CR where Python 2 does not."""
+    alpha = 'ACGTACGTACGTacgtNRYn*'
+    eol = '\r\n' if rnd.random() < 0.25 else '\n'
+    lines = []
+    if rnd.random() < 0.15:
+        lines.append(''.join(rnd.choice(alpha) for _ in range(rnd.randrange(1, 20))))
+    for r in range(rnd.randrange(1, 6)):
+        lines.append('>rec%d%s' % (r, ' some description' if rnd.random() < 0.4 else ''))
+        n = rnd.choice([0, 1, 2, 3, 4, 5, rnd.randrange(6, 91)])
+        seq = ''.join(rnd.choice(alpha) for _ in range(n))
+        w = rnd.randrange(5, 40)
+        for k in range(0, len(seq), w):
+            lines.append(seq[k:k + w])
+    if rnd.random() < 0.06:
+        lines.insert(rnd.randrange(1, len(lines) + 1), '')
+    text = eol.join(lines)
+    if rnd.random() < 0.8:
+        text += eol
+    return text
+
+
+def make_cds2pep(ref_tools, n=40):
+    """genome_tools.cds2pep (:664-675) on random FASTA files: its stdout and
+    exception (tests/test_cds2pep.py)."""
+    import tempfile
+    rnd = random.Random(20261018)
+    out = []
+    with tempfile.TemporaryDirectory() as d:
+        for i in range(n):
+            text = _cds_case(rnd)
+            path = os.path.join(d, 'c%d.fa' % i)
+            with open(path, 'wb') as fh:
+                fh.write(text.encode('ascii'))
+            res, exc, so = call(lambda: ref_tools.cds2pep(path))
+            out.append({'fasta': text, 'exc': exc, 'stdout': so})
+    return out
+
+
 def main():
     ref = reference_module()
     with open(os.path.join(HERE, 'fuzz.json'), 'w') as fh:
         json.dump(make_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'fuzz2.json'), 'w') as fh:
         json.dump(make_fuzz2(ref), fh, indent=0, sort_keys=True)
+    import genome_tools as ref_tools  # the reference's, from the same Python 3 copy
+    with open(os.path.join(HERE, 'cds2pep.json'), 'w') as fh:
+        json.dump(make_cds2pep(ref_tools), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'matches.json'), 'w') as fh:
         json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:
