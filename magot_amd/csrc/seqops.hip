@@ -4,6 +4,7 @@
 // Both are output-stationary: a lane owns 16 aligned output bytes, finds its
 // record by binary search over the offset table and reads its inputs from L2.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 
@@ -432,30 +433,45 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
 #pragma unroll
     for (int k = 0; k < kPer; ++k) iv[k] = min(cnt[lane + 64 * k], m - 1);
     uint32_t wa[kPer][3], wb[kPer][3], xa[kPer][2], xb[kPer][2];
+    // Windows without a flagged interval (most) skip the exception plane:
+    // no loads, no address math, no merge (wave-uniform).
+    const bool wexc = __builtin_amdgcn_readfirstlane(
+                          __ballot((in[0] && (rw[0].y & kOrf6ExcRow)) ||
+                                   (in[1] && (rw[1].y & kOrf6ExcRow)))) != 0;
+    auto issue = [&](auto exc_tag) {
+      constexpr bool kExc = decltype(exc_tag)::value;
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t t = lane + 64 * k;
-      const int32_t t16 = 16 * (int32_t)t;
-      const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];
-      const bool cross = (int32_t)r1.z < min(t16 + 18, wlen);
-      const auto va = __builtin_amdgcn_raw_buffer_load_b96(plane2, r0.x + 4u * t, 0, 0);
-      const auto vb =
-          __builtin_amdgcn_raw_buffer_load_b96(plane2, cross ? r1.x + 4u * t : 0xFFFFFFF0u, 0, 0);
-      const uint32_t ea = r0.w + 4u * (((r0.y & 31u) + 16u * t) >> 5);
-      const uint32_t eb = r1.w + 4u * (((r1.y & 31u) + 16u * t) >> 5);
-      const auto ua = __builtin_amdgcn_raw_buffer_load_b64(plane1, (r0.y & 32u) ? ea : 0xFFFFFFF0u, 0, 0);
-      const auto ub = __builtin_amdgcn_raw_buffer_load_b64(
-          plane1, (cross && (r1.y & 32u)) ? eb : 0xFFFFFFF0u, 0, 0);
+      for (int k = 0; k < kPer; ++k) {
+        const uint32_t t = lane + 64 * k;
+        const int32_t t16 = 16 * (int32_t)t;
+        const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];
+        const bool cross = (int32_t)r1.z < min(t16 + 18, wlen);
+        const auto va = __builtin_amdgcn_raw_buffer_load_b96(plane2, r0.x + 4u * t, 0, 0);
+        const auto vb =
+            __builtin_amdgcn_raw_buffer_load_b96(plane2, cross ? r1.x + 4u * t : 0xFFFFFFF0u, 0, 0);
 #pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        wa[k][d] = va[d];
-        wb[k][d] = vb[d];
+        for (int d = 0; d < 3; ++d) {
+          wa[k][d] = va[d];
+          wb[k][d] = vb[d];
+        }
+        if constexpr (kExc) {
+          const uint32_t ea = r0.w + 4u * (((r0.y & 31u) + 16u * t) >> 5);
+          const uint32_t eb = r1.w + 4u * (((r1.y & 31u) + 16u * t) >> 5);
+          const auto ua =
+              __builtin_amdgcn_raw_buffer_load_b64(plane1, (r0.y & 32u) ? ea : 0xFFFFFFF0u, 0, 0);
+          const auto ub = __builtin_amdgcn_raw_buffer_load_b64(
+              plane1, (cross && (r1.y & 32u)) ? eb : 0xFFFFFFF0u, 0, 0);
+          xa[k][0] = ua[0];
+          xa[k][1] = ua[1];
+          xb[k][0] = ub[0];
+          xb[k][1] = ub[1];
+        } else {
+          xa[k][0] = xa[k][1] = xb[k][0] = xb[k][1] = 0u;
+        }
       }
-      xa[k][0] = ua[0];
-      xa[k][1] = ua[1];
-      xb[k][0] = ub[0];
-      xb[k][1] = ub[1];
-    }
+    };
+    if (wexc) issue(std::true_type{});
+    else issue(std::false_type{});
     __builtin_amdgcn_sched_barrier(0);  // every window load is issued before the first is consumed
     uint32_t exact = 0;  // bit k: vector k takes the exact path below
     bool any_exc = false;
@@ -476,10 +492,13 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
       const uint32_t y1 = (b1 & (uint32_t)(mb >> 32)) | (x1 & ~(uint32_t)(mb >> 32));
       if (cross && (int32_t)row[iv[k] + 2].z < et) exact |= 1u << k;
       // exception bits of positions 0..17: bit j set = base j not ACGTacgt
-      const uint32_t ma = j0 >= 32 ? 0u : ~0u << j0;
-      const uint32_t va = funnel4(xa[k][1], xa[k][0], ((r0.y & 31u) + 16u * t) & 31u);
-      const uint32_t vb = funnel4(xb[k][1], xb[k][0], ((r1.y & 31u) + 16u * t) & 31u);
-      const uint32_t ex = (vb & ma) | (va & ~ma);
+      uint32_t ex = 0;
+      if (wexc) {
+        const uint32_t ma = j0 >= 32 ? 0u : ~0u << j0;
+        const uint32_t va = funnel4(xa[k][1], xa[k][0], ((r0.y & 31u) + 16u * t) & 31u);
+        const uint32_t vb = funnel4(xb[k][1], xb[k][0], ((r1.y & 31u) + 16u * t) & 31u);
+        ex = (vb & ma) | (va & ~ma);
+      }
       any_exc |= ex != 0;
       xa[k][0] = ex;  // reused below
       // cidx byte i = codes of positions i, i+1, i+2 = bits [2i, 2i+6)
