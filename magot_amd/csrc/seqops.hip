@@ -506,10 +506,13 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t z = j == 0 ? y0 : funnel4(y1, y0, 8u * j);
-        // four bit-field extracts and three shift-ors
-        const uint32_t lo = __builtin_amdgcn_ubfe(z, 0, 6) | (__builtin_amdgcn_ubfe(z, 2, 6) << 8);
-        const uint32_t hi = __builtin_amdgcn_ubfe(z, 4, 6) | (__builtin_amdgcn_ubfe(z, 6, 6) << 8);
-        o[j] = lo | (hi << 16);
+        // byte k = bits [2k, 2k+6) of z: two full-rate 24-bit multiplies make
+        // non-overlapping copies of the low 12 bits (shifts 0 and 12 for
+        // bytes 0 and 2, 6 and 18 for bytes 1 and 3), then two masks
+        const uint32_t z12 = z & 0xFFFu;
+        uint32_t ev = __umul24(z12, 0x1001u), od = __umul24(z12, 0x40040u);
+        __asm__("" : "+v"(ev), "+v"(od));  // kept as v_mul_u32_u24
+        o[j] = (ev & 0x003F003Fu) | (od & 0x3F003F00u);
       }
       s_stage[wave][t] = make_uint4(o[0], o[1], o[2], o[3]);
     }
@@ -525,8 +528,11 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
           uint4 c = s_stage[wave][t];
           uint32_t* const cw = reinterpret_cast<uint32_t*>(&c);
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            cw[j] |= ((__umul24((inv >> (4 * j)) & 15u, 0x204081u) & 0x01010101u) << 6);
+          for (int j = 0; j < 4; ++j) {
+            uint32_t sp = __umul24((inv >> (4 * j)) & 15u, 0x204081u);  // bit k -> bit 8k
+            __asm__("" : "+v"(sp));  // not folded with the shift into a quarter-rate v_mul_lo
+            cw[j] |= (sp & 0x01010101u) << 6;
+          }
           s_stage[wave][t] = c;
         }
       }
