@@ -460,7 +460,10 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   // 2 / 4 / 16 / 64 / 256 blocks -0.5 / -0.5 / -0.7 / +0.8 / +5 % per step
   // against round-robin; one contiguous run per XCD +7 %.  Complete groups of
   // 8 runs only, the tail keeps the identity order (a bijection).
-  constexpr uint32_t kXcdRun = 16;
+#ifndef MAGOT_EXP_XCD_RUN
+#define MAGOT_EXP_XCD_RUN 16
+#endif
+  constexpr uint32_t kXcdRun = MAGOT_EXP_XCD_RUN;
   const uint32_t xb = blockIdx.x, grp = xb / (8 * kXcdRun);
   const uint32_t vb = (grp + 1) * 8 * kXcdRun <= gridDim.x
                           ? grp * 8 * kXcdRun + (xb % 8) * kXcdRun + (xb / 8) % kXcdRun : xb;
