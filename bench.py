@@ -316,7 +316,7 @@ def strong_main(args, dist, rank, local, world):
             'extract_only': {'value': total * args.steps / el_kernel,
                              'ms_per_step': el_kernel / args.steps * 1e3},
             'genome_broadcast_s': t_bcast,
-            'settle': settled,
+            'settle': settled, 'device': ctx.info(),
             'lpt_imbalance': float(load.max() / max(load.mean(), 1.0) - 1.0),
             'parity': parity,
             'phases_s': {'generate': t_gen},
@@ -413,7 +413,7 @@ def orf6_main(args, dist, rank, local, world):
                          'kernel_ms': k_o6,
                          'extract_kernel_ms_nucleotide_only': k_ex,
                          'algorithmic_bytes_per_step': alg},
-            'cpu_baseline': cpu, 'settle': settled, 'parity': parity,
+            'cpu_baseline': cpu, 'settle': settled, 'device': ctx.info(), 'parity': parity,
             'phases_s': {'generate': t_gen},
         }
         print(json.dumps(rec), flush=True)
@@ -571,7 +571,7 @@ def main():
                          'kernel_ms_max_rank': kernel_ms_max,
                          'algorithmic_bytes_per_launch': alg_bytes},
             'cpu_baseline': cpu,
-            'settle': settled,
+            'settle': settled, 'device': ctx.info(),
             'parity': parity if ok_all == 0 else 'MISMATCH on %d rank(s)' % int(ok_all),
             'phases_s': {'generate': t_gen, 'pack_h2d': t_pack, 'plan_h2d': t_plan,
                          'execute_fetch_d2h': t_fetch},

@@ -167,6 +167,11 @@ int magot_plan_execute(magot_ctx* ctx, magot_plan* p);
 /* Block until the context stream is idle. */
 int magot_ctx_sync(magot_ctx* ctx);
 
+/* Device facts of a context: compute units, and the extraction kernel's
+ * resident workgroups per CU as launched (its occupancy cap included).  Any
+ * pointer may be NULL.  No reference counterpart (diagnostics for bench.py). */
+int magot_ctx_info(const magot_ctx* ctx, int* n_cu, int* extract_blocks_per_cu);
+
 /* Copy outputs to caller buffers (synchronous).  Any pointer may be NULL to
  * skip it.  nuc_off / pep_off receive n_tx+1 prefix offsets. */
 int magot_plan_fetch(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off,

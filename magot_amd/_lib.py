@@ -25,7 +25,7 @@ RC_BIT = np.uint64(1 << 63)
 # Every symbol include/magot.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     'magot_abi_version', 'magot_last_error', 'magot_device_count',
-    'magot_ctx_create', 'magot_ctx_destroy', 'magot_ctx_sync',
+    'magot_ctx_create', 'magot_ctx_destroy', 'magot_ctx_sync', 'magot_ctx_info',
     'magot_genome_load', 'magot_genome_stats', 'magot_genome_destroy',
     'magot_plan_create', 'magot_plan_destroy', 'magot_plan_execute', 'magot_plan_fetch',
     'magot_run', 'magot_plan_time', 'magot_plan_device_outputs',
@@ -68,6 +68,8 @@ def _declare(lib):
         'magot_ctx_create': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
         'magot_ctx_destroy': (None, [_vp]),
         'magot_ctx_sync': (ctypes.c_int, [_vp]),
+        'magot_ctx_info': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_int)]),
         'magot_genome_load': (ctypes.c_int, [_vp, ctypes.POINTER(_u8p), _u64p, ctypes.c_uint32,
                                              ctypes.POINTER(_vp)]),
         'magot_genome_stats': (ctypes.c_int, [_vp, _u64p, _u64p, _u64p]),
@@ -170,6 +172,13 @@ class Context(object):
 
     def sync(self):
         check(lib().magot_ctx_sync(self.handle), 'magot_ctx_sync')
+
+    def info(self):
+        """{'n_cu', 'extract_blocks_per_cu'} of the device (magot_ctx_info)."""
+        n_cu, blocks = ctypes.c_int(), ctypes.c_int()
+        check(lib().magot_ctx_info(self.handle, ctypes.byref(n_cu), ctypes.byref(blocks)),
+              'magot_ctx_info')
+        return {'n_cu': n_cu.value, 'extract_blocks_per_cu': blocks.value}
 
     def close(self):
         if self.handle:

@@ -205,6 +205,16 @@ void magot_ctx_destroy(magot_ctx* ctx) {
   delete ctx;
 }
 
+int magot_ctx_info(const magot_ctx* ctx, int* n_cu, int* extract_blocks_per_cu) {
+  if (!ctx) {
+    set_error("magot_ctx_info: null context");
+    return MAGOT_ERR_ARG;
+  }
+  if (n_cu) *n_cu = ctx->n_cu;
+  if (extract_blocks_per_cu) *extract_blocks_per_cu = ctx->blocks_per_cu;
+  return MAGOT_OK;
+}
+
 int magot_ctx_sync(magot_ctx* ctx) {
   if (int rc = bind(ctx)) return rc;
   MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
