@@ -256,12 +256,22 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
   // byte offsets of the quads in read order, one per byte: 12 * ((s + rj) & 3)
   const uint32_t qo = __builtin_amdgcn_alignbit(0x24180C00u, 0x24180C00u, 8u * rj);
   uint32_t r[4];
+  // every codon index in flight before the first table read
+  uint32_t c[4][4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const uint8_t* const qs = src + ((qo >> (8 * s)) & 0xFFu);
-    // three ops per quad: two byte pairs, then one perm
-    const uint32_t lo = (uint32_t)tb[qs[0]] | ((uint32_t)tb[qs[3]] << 8);
-    const uint32_t hi = (uint32_t)tb[qs[6]] | ((uint32_t)tb[qs[9]] << 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c[s][i] = qs[3 * i];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    // three ops per quad: two byte pairs, then one perm; a quad of an
+    // all-'-' iteration is packed in reverse byte order (the reversal below
+    // is then a register renaming)
+    constexpr int k0 = kMode == 1 ? 3 : 0, k1 = kMode == 1 ? 2 : 1;
+    const uint32_t lo = (uint32_t)tb[c[s][k0]] | ((uint32_t)tb[c[s][k1]] << 8);
+    const uint32_t hi = (uint32_t)tb[c[s][3 - k1]] | ((uint32_t)tb[c[s][3 - k0]] << 8);
     r[s] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
   }
   uint32_t o[4];  // o[d] = r[(d - rj) & 3]: rotate by 2, then by 1
@@ -274,7 +284,14 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
     o[2] = j1 ? t1 : t2;
     o[3] = j1 ? t2 : t3;
   }
-  if (minus) {
+  if constexpr (kMode == 1) {  // bytes already reversed: reverse the words
+    uint32_t t = o[0];
+    o[0] = o[3];
+    o[3] = t;
+    t = o[1];
+    o[1] = o[2];
+    o[2] = t;
+  } else if (minus) {
     const uint32_t t0 = o[0], t1 = o[1];
     o[0] = __builtin_amdgcn_perm(0u, o[3], 0x00010203u);
     o[1] = __builtin_amdgcn_perm(0u, o[2], 0x00010203u);
