@@ -43,7 +43,8 @@ namespace {
 constexpr int kGuard = 4;  // LDS words before codes[0] (codons of residue chunk 0 may start < 0)
 
 struct WaveLds {
-  uint4 ex[kExonCap];                     // {anchor lo, anchor hi, end (tile-rel), flags}
+  uint4 ex[kExonCap];                     // {plane byte offset, anchor lo, end (tile-rel), flags}
+  uint32_t vb[kExonCap];                  // reverse-forward rows: forward-plane byte offset
   int64_t tn[kTxCap + 1];                 // record codon-0 output position, tile-relative
   int64_t tp[kTxCap + 1];                 // record first residue, relative to the tile's Q0
   uint32_t codes_g[kGuard + kSlots + 8];  // 2-bit codes per chunk (histogram scratch first)
@@ -55,6 +56,11 @@ struct WaveLds {
 constexpr uint32_t kFlagRc = 1u;
 constexpr uint32_t kFlagExc = 2u;      // touches an exception run
 constexpr uint32_t kFlagSlowLit = 4u;  // ... one without a literal class (run-list path)
+// '-' interval without exceptions: the fast path reads it from the forward
+// plane, descending (vb, shift in bits 13..15), and reverse-complements the
+// chunk in registers; its mirror anchor stays for the slow path and for
+// chunks whose other segment is not reverse-forward
+constexpr uint32_t kFlagRevFwd = 32u;
 
 __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
   return __builtin_amdgcn_alignbit(hi, lo, sh);  // (hi:lo >> sh)[31:0], sh in 0..31
@@ -358,9 +364,15 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
       const int64_t e = (int64_t)(o1 - d.T0);
       const uint64_t U = row_anchor(gw, o0, o1, d.T0, span);
       const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
+      // reverse-forward: chunk c's 16 bytes are the forward bases V - 16c ..
+      // V - 16c + 15, reversed and complemented (V = gs + len - 16 + s)
+      const bool revfwd = (gw & kRcBit) && !(gw & kExcBit);
+      const int64_t V = (int64_t)(gw & ~kExFlagBits) + (int64_t)(o1 - d.T0) - 16;
       const uint32_t fl = ((gw & kRcBit) ? kFlagRc : 0u) | ((gw & kExcBit) ? kFlagExc : 0u) |
                           ((gw & kSlowLitBit) ? kFlagSlowLit : 0u) | ((uint32_t)(U & 7) << 8) |
-                          ((uint32_t)(U >> 32) & 1u) << 12;
+                          ((uint32_t)(U >> 32) & 1u) << 12 |
+                          (revfwd ? kFlagRevFwd | ((uint32_t)(V & 7) << 13) : 0u);
+      L.vb[j] = (uint32_t)(V >> 3) << 2;
       // byte offset of the plane word holding tile byte 0's base (mod 2^32:
       // U may wrap below 0, the chunks the row serves do not); chunk c reads
       // its window at bN + 8c, funnel shift 4 * (U & 7).  The slow path takes
@@ -427,6 +439,13 @@ __device__ __forceinline__ uint2 seg_masks(uint32_t n1) {
   return make_uint2(mlo, mhi);
 }
 
+// Eight nibbles reversed, codes complemented (A<->T, C<->G: code ^ 3; the
+// soft-mask bit kept).  For nibbles without the exception bit only.
+__device__ __forceinline__ uint32_t revcomp8(uint32_t w) {
+  const uint32_t b = __builtin_amdgcn_perm(0u, w, 0x00010203u);  // bytes reversed
+  return bfi(0x0F0F0F0Fu, b >> 4, b << 4) ^ 0x33333333u;           // nibbles in each byte
+}
+
 __device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, const uint2* masks,
                                            uint32_t& x0, uint32_t& x1) {
   const uint32_t sa = (mt >> 6) & 28u, sb = (mt >> 14) & 28u;  // 4 * (u & 7)
@@ -434,7 +453,7 @@ __device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, const 
   const uint32_t b0 = funnel(B.y, B.x, sb), b1 = funnel(B.z, B.y, sb);
   // n1 = bytes from segment A (16 when the chunk is one segment): masks from
   // the wave's LDS table (seg_masks)
-  const uint2 m = masks[(mt >> 24) & 31u];
+  const uint2 m = masks[(mt >> 24) & 63u];
   x0 = bfi(m.x, a0, b0);
   x1 = bfi(m.y, a1, b1);
 }
@@ -442,7 +461,7 @@ __device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, const 
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   __shared__ WaveLds s_wave[kWaves];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[64];
-  __shared__ uint2 s_mask[17];
+  __shared__ uint2 s_mask[34];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -478,7 +497,11 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(a.lut[i]), "i"(i));
     if (lane < 16) reinterpret_cast<uint32_t*>(s_lut)[lane] = (uint32_t)v;
-    if (lane <= 16) s_mask[lane] = seg_masks((uint32_t)lane);  // identical in every wave
+    // identical in every wave: [n] low n nibbles, [17 + n] high n nibbles
+    if (lane < 34) {
+      const uint2 lo = seg_masks(lane <= 16 ? (uint32_t)lane : (uint32_t)(33 - lane));
+      s_mask[lane] = lane <= 16 ? lo : make_uint2(~lo.x, ~lo.y);
+    }
   }
   if (lane < kGuard) {
     L.codes_g[lane] = 0;
@@ -497,8 +520,8 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   // ---- nucleotide chunks: issue every window load first -------------------
   const __amdgpu_buffer_rsrc_t nib_rs = plane_rsrc(a.nib);
   uint3 wA[kLaneChunks], wB[kLaneChunks];
-  uint32_t meta[kLaneChunks];  // bit0 active, 4 slow, 8..10 u_A & 7, 16..18 u_B & 7,
-                               // 24..28 bytes from segment A
+  uint32_t meta[kLaneChunks];  // bit0 active, 2 reversed, 4 slow, 8..10 / 16..18 nibble
+                               // shift of the A / B window, 24..29 mask index
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) {
     const int c = min(lane + 64 * k, g.n_all - 1);  // clamped: inactive lanes redo a chunk
@@ -512,16 +535,37 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     const uint32_t fb = two ? Y.w : X.w;
     const bool slow = ((X.w | fb) & kFlagSlowLit) != 0 || (two && (int)Y.z < cend) ||
                       (a.outputs & kDebugSlowNuc);
-    const uint32_t offa = X.x + 8u * (uint32_t)c;
-    const uint32_t offb = two ? Y.x + 8u * (uint32_t)c : offa;
-    meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (slow ? 16u : 0u) |
-              (X.w & 0x700u) | ((fb & 0x700u) << 8) | ((uint32_t)(two ? n1 : 16) << 24);
+    // both segments reverse-forward (or one that is): forward-plane windows,
+    // descending; the merged chunk is reverse-complemented below.  A chunk
+    // whose other segment is not reverse-forward reads the mirror instead.
+    const bool rev = (X.w & fb & kFlagRevFwd) != 0;
+    const uint32_t c8 = 8u * (uint32_t)c;
+    // every candidate offset computed unconditionally (selects, no branches
+    // around LDS reads)
+    uint32_t fa = X.x + c8, ra = L.vb[i] - c8;
+    const uint32_t ib = (uint32_t)min(i + 1, (int)d.m - 1) & (kExonCap - 1);  // < kExonCap
+    uint32_t fb2 = Y.x + c8, rb = L.vb[ib] - c8;
+    __asm__("" : "+v"(fa), "+v"(ra), "+v"(fb2), "+v"(rb));
+    const uint32_t offa = rev ? ra : fa;
+    const uint32_t offb = two ? (rev ? rb : fb2) : offa;
+    const uint32_t sha = (rev ? X.w >> 5 : X.w) & 0x700u, shb = (rev ? fb >> 5 : fb) & 0x700u;
+    // mask index: segment A's bytes are the low n1 nibbles, or (reversed) the
+    // high n1 nibbles (s_mask[17 + n1])
+    const uint32_t mi = (uint32_t)(two ? n1 : 16) + (rev ? 17u : 0u);
+    meta[k] = ((lane + 64 * k) < g.n_all ? 1u : 0u) | (rev ? 4u : 0u) | (slow ? 16u : 0u) |
+              sha | (shb << 8) | (mi << 24);
     wA[k] = load_window(nib_rs, offa);
     wB[k] = load_window(nib_rs, offb);
   }
   uint32_t x0k[kLaneChunks], x1k[kLaneChunks];
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) fast_chunk(wA[k], wB[k], meta[k], s_mask, x0k[k], x1k[k]);
+  for (int k = 0; k < kLaneChunks; ++k) {
+    fast_chunk(wA[k], wB[k], meta[k], s_mask, x0k[k], x1k[k]);
+    const uint32_t r0 = revcomp8(x1k[k]), r1 = revcomp8(x0k[k]);
+    const bool rv = (meta[k] & 4u) != 0;
+    x0k[k] = rv ? r0 : x0k[k];
+    x1k[k] = rv ? r1 : x1k[k];
+  }
   uint32_t slow_any = 0, exc_any = 0;
 #pragma unroll
   for (int k = 0; k < kLaneChunks; ++k) {
