@@ -525,6 +525,57 @@ def test_every_byte_class_both_strands_vs_oracle():
     dev.close()
 
 
+@pytest.mark.parametrize('max_len', [20, 70, 400])
+def test_reverse_forward_segments_vs_oracle(max_len):
+    """extract_kernel's reverse-forward path (v19): '-' intervals without
+    exceptions read the forward plane descending and are reverse-complemented
+    in registers; '-' intervals over N runs or IUPAC bytes read the mirror;
+    chunks whose two segments differ in strand or in path take the mirror for
+    their '-' segment.  Per-interval random strands inside records, short
+    intervals (two- and three-segment chunks), soft-masked runs, contig
+    starts and ends, several contigs."""
+    rng = np.random.default_rng(max_len)
+    contigs = []
+    for k, n in enumerate((30_000, 777, 45_001, 64)):
+        b = rng.choice(np.frombuffer(b'ACGTacgt', np.uint8), n)
+        for j in range(0, n, 900):  # sparse N runs and IUPAC bytes
+            if rng.random() < 0.3:
+                b[j:j + int(rng.integers(1, 40))] = ord('N')
+            if rng.random() < 0.2:
+                b[min(j + 300, n - 1)] = rng.choice(np.frombuffer(b'RYKMSWn-', np.uint8))
+        contigs.append(('c%d' % k, b.tobytes()))
+    dev = engine.DeviceGenome(contigs)
+    rows, txs = [], []
+    for t in range(900):
+        ci = int(rng.integers(0, len(contigs)))
+        clen = len(contigs[ci][1])
+        n = int(rng.integers(1, 9))
+        b = len(rows)
+        for _ in range(n):
+            ln = int(rng.integers(1, min(max_len, clen) + 1))
+            u = rng.random()
+            st = 0 if u < 0.05 else clen - ln if u < 0.1 else int(rng.integers(0, clen - ln + 1))
+            minus = bool(rng.integers(0, 2))
+            rows.append(((st | (1 << 63)) if minus else st, ci, ln))
+        txs.append((b, n, 0))
+    ex = np.array(rows, dtype=engine.EXON_DTYPE)
+    tx = np.array(txs, dtype=engine.TX_DTYPE)
+    plan = engine.ExtractionPlan(dev, ex, tx)
+    nuc, noff, pep, poff = plan.run()
+    for r, (b, n, _) in enumerate(txs):
+        segs = []
+        for sr, ci, ln in rows[b:b + n]:
+            st = sr & ~(1 << 63)
+            s = contigs[ci][1][st:st + ln].decode('latin-1')
+            segs.append(mo.reverse_complement(s) if sr >> 63 else s)
+        want = ''.join(segs)
+        assert nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1') == want, r
+        got = pep[int(poff[r]):int(poff[r + 1])].tobytes().decode('latin-1')
+        assert got == (mo.translate(want, trimX=False) or ''), r
+    plan.close()
+    dev.close()
+
+
 def test_orf6_fused_code_plane_boundaries_vs_oracle():
     """The fused gather's 2-bit fast path at its edges: intervals of 14-20
     bases put the second (and third) interval exactly at the 16th-18th
