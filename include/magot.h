@@ -257,17 +257,25 @@ void magot_orf6_destroy(magot_orf6* o);
  * and de-duplication, v2 parent hierarchy, Base/Parent typing), keeps the
  * AnnotationSet model (global ID lookup: last matching type in sorted order,
  * genome.py:536-544) and lowers AnnotationSet.get_fasta(feature)
- * (genome.py:578-582, 677-731; longest=False, genomic=False) to interval and
- * record tables for magot_plan_create plus a FASTA text skeleton.
+ * (genome.py:578-582, 677-731) to interval and record tables for
+ * magot_plan_create plus a FASTA text skeleton.
  * seqids / contig_lens: the GenomeSequence (genome.py:854-877) in the order
  * its contigs were given to magot_genome_load.  flags: MAGOT_GFF_PROTEIN for
- * seq_type="protein", MAGOT_GFF_ORDER_PY2 for CPython 2.7 dict order.
+ * seq_type="protein", MAGOT_GFF_ORDER_PY2 for CPython 2.7 dict order,
+ * MAGOT_GFF_GENOMIC for genomic=True (genome.py:680-682: one '+' interval per
+ * feature over its get_coords() span, never translated, so the plan is a
+ * nucleotide plan whatever MAGOT_GFF_PROTEIN says), MAGOT_GFF_LONGEST for
+ * longest=True (genome.py:720-724: the child record with the longest
+ * sequence, the later one on a tie; nucleotide only, as a protein's length
+ * depends on the leading-'X' trim, i.e. on the genome).
  * Returns MAGOT_ERR_UNSUPPORTED when the input would take one of the
  * reference's diagnostic paths (prints, None, exceptions): the caller then
  * uses the object path, which reproduces them.
  */
 #define MAGOT_GFF_PROTEIN 1u
 #define MAGOT_GFF_ORDER_PY2 2u
+#define MAGOT_GFF_LONGEST 4u
+#define MAGOT_GFF_GENOMIC 8u
 typedef struct magot_gffplan magot_gffplan;
 int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
                    const uint64_t* contig_lens, uint32_t n_contigs, const char* feature,

@@ -44,6 +44,8 @@ EXPORTS = (
 ERR_UNSUPPORTED = -5
 GFF_PROTEIN = 1
 GFF_ORDER_PY2 = 2
+GFF_LONGEST = 4
+GFF_GENOMIC = 8
 
 
 class MagotError(RuntimeError):

@@ -798,6 +798,8 @@ struct magot_gffplan : magot::Lowered {
 namespace magot {
 namespace {
 
+void append_lowered(Lowered& all, const Lowered& part);
+
 struct Lowering {
   Lowered& P;
   const Model& M;
@@ -805,6 +807,7 @@ struct Lowering {
   const std::vector<int64_t>& contig_idx;  // seqid -> contig (-1: missing)
   const uint64_t* contig_len;
   const std::vector<uint32_t>& id_of_feat;  // the ID a feature was stored under
+  bool longest = false;  // get_fasta(longest=True), applied at the top level only
 
   void text(sv s) {
     if (s.empty()) return;
@@ -890,6 +893,7 @@ struct Lowering {
       P.txs.push_back(t);
       return 1;
     }
+    if (longest) return fasta_longest(F);
     uint64_t n = 0;
     for (uint32_t c : F.children) {
       const int64_t o = M.lookup(c);
@@ -898,6 +902,105 @@ struct Lowering {
       n += fasta((uint32_t)o, first_in_join && n == 0);
     }
     return n;
+  }
+
+  // Parent branch with longest=True (genome.py:711-724): each child's
+  // get_fasta (longest=False) is a candidate unless it is ""; the key of a
+  // candidate string is len("".join(seq.split('\n')[1:])), a dict keyed by it
+  // keeps the later candidate of a length, and the maximal key wins.  No
+  // candidate: max() of an empty list, ValueError.
+  uint64_t fasta_longest(const Feature& F) {
+    if (protein) throw Unsupported();  // a peptide's length depends on the genome (trimX)
+    Lowered best;
+    uint64_t best_key = 0;
+    bool have = false;
+    for (uint32_t c : F.children) {
+      const int64_t o = M.lookup(c);
+      if (o < 0) throw Unsupported();
+      if (M.feats[(size_t)o].base) throw Unsupported();  // mixed children: print
+      Lowered T;
+      Lowering sub{T, M, protein, contig_idx, contig_len, id_of_feat};
+      if (sub.fasta((uint32_t)o, true) == 0) continue;  // child_fasta == ""
+      const uint64_t key = candidate_key(T);
+      if (!have || key >= best_key) {
+        best = std::move(T);
+        best_key = key;
+        have = true;
+      }
+    }
+    if (!have) throw Unsupported();
+    append_lowered(P, best);
+    return 1;
+  }
+
+  // Characters of a lowered candidate string that are not '\n', after its
+  // first line (nucleotide payloads: the records' interval lengths).
+  static uint64_t candidate_key(const Lowered& T) {
+    uint64_t n = 0, first_line = 0;
+    bool in_first = true;
+    for (const Piece& pc : T.pieces) {
+      if (pc.rec >= 0) {
+        const magot_tx& t = T.txs[(size_t)pc.rec];
+        uint64_t len = 0;
+        for (uint64_t e = t.exon_begin; e < t.exon_begin + t.n_exons; ++e) len += T.exons[e].len;
+        n += len;
+        if (in_first) first_line += len;
+        continue;
+      }
+      for (uint64_t k = pc.off; k < pc.off + pc.len; ++k) {
+        if (T.text[k] == '\n') {
+          in_first = false;
+          continue;
+        }
+        ++n;
+        if (in_first) ++first_line;
+      }
+    }
+    return n - first_line;
+  }
+
+  // get_coords() (genome.py:663-675): min and max over the children's coords,
+  // recursively.  A parent without children returns None, and the caller's
+  // [0] raises TypeError.
+  void coords(const Feature& F, int64_t& lo, int64_t& hi) const {
+    if (F.children.empty()) throw Unsupported();
+    for (uint32_t c : F.children) {
+      const int64_t o = M.lookup(c);
+      if (o < 0) throw Unsupported();  // KeyError
+      const Feature& C = M.feats[(size_t)o];
+      if (C.base) {
+        lo = std::min(lo, C.lo);
+        hi = std::max(hi, C.hi);
+      } else {
+        coords(C, lo, hi);
+      }
+    }
+  }
+
+  // genomic=True (genome.py:680-682): ">" + ID + "\n" + contig[lo-1:hi] + "\n",
+  // forward strand, never translated.
+  void genomic(uint32_t fi) {
+    const Feature& F = M.feats[fi];
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    coords(F, lo, hi);
+    const int64_t cix = contig_idx[F.seqid];
+    if (cix < 0) throw Unsupported();  // KeyError
+    uint64_t st, ln;
+    slice(lo - 1, hi, (int64_t)contig_len[cix], &st, &ln);
+    if (ln >= 0xFFFFFFFFull) throw Unsupported();
+    header(M.ids.strs[id_of_feat[fi]]);
+    magot_tx t;
+    t.exon_begin = P.exons.size();
+    t.n_exons = 1;
+    t.flags = 0;
+    magot_exon x;
+    x.start_rc = st;
+    x.contig = (uint32_t)cix;
+    x.len = (uint32_t)ln;
+    P.exons.push_back(x);
+    P.pieces.push_back({0, 0, (int64_t)P.txs.size()});
+    P.txs.push_back(t);
+    text("\n");
   }
 
 };
@@ -934,7 +1037,8 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
   }
   *out = nullptr;
   std::unique_ptr<magot_gffplan> P(new magot_gffplan());
-  P->protein = (flags & MAGOT_GFF_PROTEIN) != 0;
+  const bool genomic = (flags & MAGOT_GFF_GENOMIC) != 0;
+  P->protein = (flags & MAGOT_GFF_PROTEIN) != 0 && !genomic;  // genomic: never translated
   const bool timing = std::getenv("MAGOT_GFF_TIMING") != nullptr;
   auto now = [] { return std::chrono::steady_clock::now(); };
   auto t0 = now();
@@ -986,12 +1090,14 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
       for (size_t q; (q = next.fetch_add(1)) < n_parts && !unsupported.load();) {
         magot::Lowered& out = q ? parts[q] : *P;
         magot::Lowering L{out, M, P->protein, contig_idx, contig_lens, id_of_feat};
+        L.longest = (flags & MAGOT_GFF_LONGEST) != 0;
         try {
           for (size_t i = n_keys * q / n_parts; i < n_keys * (q + 1) / n_parts; ++i) {
             const uint32_t fi = (uint32_t)M.slot(table, keys[i]);
             if (M.feats[fi].base) throw Unsupported();  // BaseAnnotation has no get_fasta
             if (i) L.text("\n");
-            L.fasta(fi, true);
+            if (genomic) L.genomic(fi);
+            else L.fasta(fi, true);
           }
         } catch (const Unsupported&) {
           unsupported = true;

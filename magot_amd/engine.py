@@ -415,14 +415,20 @@ class GffPlan(object):
               'magot_gffplan_tables')
 
     @classmethod
-    def build(cls, gff, names, lengths, feature='gene', protein=False, order='insertion'):
+    def build(cls, gff, names, lengths, feature='gene', protein=False, order='insertion',
+              longest=False, genomic=False):
+        """``longest`` / ``genomic``: get_fasta's options (genome.py:677-724).
+        genomic=True is never translated (a nucleotide plan whatever
+        ``protein`` says); longest=True is planned for nucleotide only (None,
+        the object path, for a protein parent branch)."""
         L = _lib.lib()
         text = _text_view(gff)
         n = len(names)
         arr = (ctypes.c_char_p * max(n, 1))(*[_as_bytes(x) for x in names])
         lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
         flags = (_lib.GFF_PROTEIN if protein else 0) | \
-            (_lib.GFF_ORDER_PY2 if order == 'py2' else 0)
+            (_lib.GFF_ORDER_PY2 if order == 'py2' else 0) | \
+            (_lib.GFF_LONGEST if longest else 0) | (_lib.GFF_GENOMIC if genomic else 0)
         h = ctypes.c_void_p()
         ne, nt = ctypes.c_uint64(), ctypes.c_uint64()
         rc = L.magot_gff_plan(_text_ptr(text), len(text), arr, lens.ctypes.data_as(_lib._u64p), n,
@@ -431,7 +437,7 @@ class GffPlan(object):
         if rc == _lib.ERR_UNSUPPORTED:
             return None
         check(rc, 'magot_gff_plan')
-        return cls(h, ne.value, nt.value, protein)
+        return cls(h, ne.value, nt.value, protein and not genomic)
 
     def render(self, nuc, noff, pep, poff):
         """The FASTA text (bytes) around the fetched record payloads."""

@@ -64,13 +64,16 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
               genomic='False', order='py2', native='True'):
     """genome_tools.py:324-330.
 
-    Default arguments go through the native planner (magot_gff_plan: read_gff
-    + get_fasta lowering in C++) and one kernel launch; inputs that take one
-    of the reference's diagnostic paths, and the longest / genomic /
-    from_exons variants, use the object path (``native=False`` forces it)."""
-    if (native == 'True' and from_exons != 'True' and _literal(longest) is False and
-            _literal(genomic) is False and seq_type in ('nucleotide', 'protein')):
-        text = _gff2fasta_native(genome_sequence, gff, seq_type, order)
+    The native planner (magot_gff_plan: read_gff + get_fasta lowering in C++)
+    and one kernel launch serve the default call, genomic=True and
+    longest=True; inputs that take one of the reference's diagnostic paths,
+    longest protein parents (a peptide's length depends on the genome) and
+    from_exons use the object path (``native=False`` forces it)."""
+    lg, gm = _literal(longest), _literal(genomic)
+    if (native == 'True' and from_exons != 'True' and isinstance(lg, bool) and
+            isinstance(gm, bool) and seq_type in ('nucleotide', 'protein')):
+        text = _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=lg is True,
+                                 genomic=gm is True)
         if text is not None:
             _write_bytes(text, b'\n')
             return
@@ -85,7 +88,7 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
     _write(text + '\n')
 
 
-def _gff2fasta_native(genome_sequence, gff, seq_type, order):
+def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, genomic=False):
     """The gff2fasta text (bytes) via the native planner, the extraction
     kernel and device text assembly, or None when the planner declines."""
     if order not in ('py2', 'insertion'):
@@ -100,12 +103,12 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order):
     names = dev.names
     protein = seq_type == 'protein'
     plan = engine.GffPlan.build(genome.read_buffer(gff), names, [int(x) for x in dev.lengths],
-                                protein=protein, order=order)
+                                protein=protein, order=order, longest=longest, genomic=genomic)
     if plan is None:
         return None
     try:
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
-                                   engine.OUT_PEP if protein else engine.OUT_NUC)
+                                   engine.OUT_PEP if plan.protein else engine.OUT_NUC)
         text = engine.FastaText(plan, ex)
         try:
             ex.execute()

@@ -41,11 +41,13 @@ def _payloads(plan, seqs):
     return enc(nuc), np.array(noff, np.uint64), enc(pep), np.array(poff, np.uint64)
 
 
-def native_gff2fasta(fasta, gff, seq_type='nucleotide', order='insertion'):
+def native_gff2fasta(fasta, gff, seq_type='nucleotide', order='insertion', longest=False,
+                     genomic=False):
     gs = G.GenomeSequence(fasta)
     names = list(gs)
     plan = engine.GffPlan.build(G.ensure_file(gff).read(), names, [len(gs[n]) for n in names],
-                                protein=seq_type == 'protein', order=order)
+                                protein=seq_type == 'protein', order=order, longest=longest,
+                                genomic=genomic)
     if plan is None:
         return None
     text = plan.render(*_payloads(plan, [gs[n] for n in names]))
@@ -207,3 +209,107 @@ def test_native_plan_chunked_declines(monkeypatch):
     assert engine.GffPlan.build(good, list(gs), [400], protein=True) is not None
     bad = good + 'c1\tx\tgene\t1\tten\t.\t+\t.\tID=gz\n'
     assert engine.GffPlan.build(bad, list(gs), [400], protein=True) is None
+
+
+# ---------------------------------------------------------------------------
+# get_fasta(longest=True) and get_fasta(genomic=True) through the native
+# planner (genome.py:680-682, 711-724), on the randomised inputs whose
+# reference outputs tests/golden/fuzz*.json hold (renamed IDs, reversed and
+# past-end coordinates, mixed strands, UTR / exon children, GTF hierarchies)
+# ---------------------------------------------------------------------------
+
+def _fuzz_inputs():
+    import json
+    import os
+    out = []
+    for name in ('fuzz.json', 'fuzz2.json'):
+        for rec in json.load(open(os.path.join(goldlib.HERE, name))):
+            out.append((rec['fasta'], rec['gff']))
+    return out
+
+
+FUZZ_INPUTS = _fuzz_inputs()
+
+
+def _oracle_or_diag(fasta, gff, **kw):
+    import io
+    out = io.StringIO()  # the oracle's diagnostic prints
+    try:
+        text = mo.gff2fasta(fasta, gff, out=out, **kw)
+    except Exception:
+        return None, True
+    return text, bool(out.getvalue())
+
+
+@pytest.mark.parametrize('i', range(len(FUZZ_INPUTS)))
+def test_native_longest_and_genomic_match_oracle(i):
+    fasta, gff = FUZZ_INPUTS[i]
+    calls = [dict(seq_type='nucleotide', longest=True), dict(seq_type='nucleotide', genomic=True),
+             dict(seq_type='protein', genomic=True),
+             dict(seq_type='protein', genomic=True, longest=True)]
+    for kw in calls:
+        for order in ('insertion', 'py2'):
+            got = native_gff2fasta(fasta, gff, order=order, **kw)
+            want, diag = _oracle_or_diag(fasta, gff, order=order, **kw)
+            if got is None:
+                assert diag, ('declined without a diagnostic path', kw, order)
+                continue
+            assert not diag, ('planned an input with a diagnostic path', kw, order)
+            assert got == want, (kw, order)
+
+
+def test_native_longest_and_genomic_plan_most_inputs():
+    """The native planner serves most of those calls (the rest hit a
+    reference diagnostic path and go to the object path)."""
+    planned = 0
+    for fasta, gff in FUZZ_INPUTS:
+        for kw in (dict(longest=True), dict(genomic=True)):
+            planned += native_gff2fasta(fasta, gff, 'nucleotide', 'py2', **kw) is not None
+    assert planned >= len(FUZZ_INPUTS) // 2, planned
+
+
+def test_native_longest_synthetic():
+    """Genes with 1-4 transcripts of random CDS sets on both strands, some of
+    equal length (a tie: the later transcript wins), genes without
+    transcripts, in GFF3 and in both record orders."""
+    rng = np.random.default_rng(33)
+    contig = ''.join(rng.choice(list('ACGTacgtN'), 60_000))
+    fasta = '>c1\n' + contig + '\n'
+    rows = []
+    for g in range(150):
+        lo = int(rng.integers(1, 55_000))
+        st = '+-'[int(rng.integers(0, 2))]
+        rows.append('c1\tx\tgene\t%d\t%d\t.\t%s\t.\tID=g%d' % (lo, lo + 4000, st, g))
+        shared = None
+        for m in range(int(rng.integers(0, 5))):
+            rows.append('c1\tx\tmRNA\t%d\t%d\t.\t%s\t.\tID=g%d.m%d;Parent=g%d'
+                        % (lo, lo + 4000, st, g, m, g))
+            if shared is not None and rng.random() < 0.3:
+                cds = shared  # same intervals: same length, a tie
+            else:
+                cds = sorted({(int(a), int(a) + int(rng.integers(3, 300)))
+                              for a in rng.integers(lo, lo + 3500, size=int(rng.integers(1, 6)))})
+            shared = cds
+            for k, (a, b) in enumerate(cds):
+                rows.append('c1\tx\tCDS\t%d\t%d\t.\t%s\t0\tID=cds.g%d.m%d;Parent=g%d.m%d'
+                            % (a, b, st, g, m, g, m))
+    gff = '\n'.join(rows) + '\n'
+    for order in ('py2', 'insertion'):
+        got = native_gff2fasta(fasta, gff, 'nucleotide', order, longest=True)
+        assert got is not None
+        assert got == mo.gff2fasta(fasta, gff, seq_type='nucleotide', order=order, longest=True)
+        gen = native_gff2fasta(fasta, gff.replace('\tID=g7\n', '\tID=g7\n'), 'protein', order,
+                               genomic=True)
+        want, diag = _oracle_or_diag(fasta, gff, seq_type='protein', order=order, genomic=True)
+        assert (gen is None) == diag  # genes without transcripts: get_coords() is None
+        if gen is not None:
+            assert gen == want
+
+
+def test_native_longest_protein_declines():
+    gs = G.GenomeSequence('>c1\nATGAAACCCGGGTTTTAA\n')
+    gff = ('c1\tx\tgene\t1\t18\t.\t+\t.\tID=g1\n'
+           'c1\tx\tmRNA\t1\t18\t.\t+\t.\tID=m1;Parent=g1\n'
+           'c1\tx\tCDS\t1\t18\t.\t+\t0\tID=c1;Parent=m1\n')
+    assert engine.GffPlan.build(gff, list(gs), [18], protein=True, longest=True) is None
+    assert engine.GffPlan.build(gff, list(gs), [18], protein=False, longest=True) is not None
