@@ -1,0 +1,38 @@
+"""Times gff2fasta's longest=True and genomic=True variants on the native path
+over the files of an e2e_cli.py run (C3 by default), each in this process
+after one warm call of the default variant (device start-up excluded).
+Correctness of these variants is pinned by tests/test_gffplan.py (oracle) and
+tests/test_fuzz.py (reference outputs); here only time and size are reported.
+
+    python scripts/e2e_variants.py [--dir /tmp/magot_e2e]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from magot_amd import genome_tools  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--dir', default='/tmp/magot_e2e')
+    a = ap.parse_args()
+    fa, gf = os.path.join(a.dir, 'genome.fa'), os.path.join(a.dir, 'ann.gff3')
+    genome_tools._gff2fasta_native(fa, gf, 'nucleotide', 'py2')  # warm: device start-up
+    rec = {}
+    for name, kw in (('default_nucleotide', {}), ('longest_nucleotide', {'longest': True}),
+                     ('genomic', {'genomic': True})):
+        t = time.perf_counter()
+        text = genome_tools._gff2fasta_native(fa, gf, 'nucleotide', 'py2', **kw)
+        rec[name] = {'s': time.perf_counter() - t, 'native': text is not None,
+                     'bytes': None if text is None else int(len(text)) + 1}
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == '__main__':
+    main()

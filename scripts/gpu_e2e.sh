@@ -8,4 +8,6 @@ MAGOT_GENOME_TIMING=1 MAGOT_GFF_TIMING=1 timeout -k 10 900 python scripts/e2e_cl
 cat $OUT/e2e_protein.json; cat $OUT/e2e.err
 MAGOT_GENOME_TIMING=1 MAGOT_GFF_TIMING=1 timeout -k 10 300 python scripts/e2e_cli.py --config C3 --seq-type protein --whole > $OUT/e2e_whole.json 2> $OUT/e2e_whole.err || { tail -20 $OUT/e2e_whole.err; exit 1; }
 cat $OUT/e2e_whole.json; cat $OUT/e2e_whole.err
+timeout -k 10 300 python scripts/e2e_variants.py > $OUT/e2e_variants.json 2> $OUT/e2e_variants.err || { tail -20 $OUT/e2e_variants.err; exit 1; }
+cat $OUT/e2e_variants.json
 rm -rf /tmp/magot_e2e
