@@ -266,8 +266,10 @@ void magot_orf6_destroy(magot_orf6* o);
  * feature over its get_coords() span, never translated, so the plan is a
  * nucleotide plan whatever MAGOT_GFF_PROTEIN says), MAGOT_GFF_LONGEST for
  * longest=True (genome.py:720-724: the child record with the longest
- * sequence, the later one on a tie; nucleotide only, as a protein's length
- * depends on the leading-'X' trim, i.e. on the genome).
+ * sequence, the later one on a tie).  For protein the lengths depend on the
+ * leading-'X' trim, i.e. on the genome: every candidate is planned and
+ * magot_gffplan_render picks (magot_gffplan_selections > 0; such a plan has
+ * no device text assembly).
  * Returns MAGOT_ERR_UNSUPPORTED when the input would take one of the
  * reference's diagnostic paths (prints, None, exceptions): the caller then
  * uses the object path, which reproduces them.
@@ -288,6 +290,8 @@ int magot_gffplan_tables(const magot_gffplan* p, magot_exon* exons, magot_tx* tx
 int magot_gffplan_render(const magot_gffplan* p, const uint8_t* nuc, const uint64_t* noff,
                          const uint8_t* pep, const uint64_t* poff, uint8_t* out, uint64_t cap,
                          uint64_t* out_len);
+/* Number of longest=True protein choices the render makes (0: none). */
+int magot_gffplan_selections(const magot_gffplan* p, uint64_t* n_groups);
 void magot_gffplan_destroy(magot_gffplan* p);
 
 /*

@@ -1221,7 +1221,8 @@ int magot_fasta_text_create(magot_ctx* ctx, const magot_gffplan* gp, const magot
   bool protein = false;
   uint64_t n_rec = 0;
   if (!gffplan_units(gp, &text, &units, &protein, &n_rec)) {
-    set_error("magot_fasta_text_create: too many records");
+    set_error("magot_fasta_text_create: too many records, or longest=True protein choices "
+              "(magot_gffplan_selections; render those on the host)");
     return MAGOT_ERR_ARG;
   }
   if (n_rec != p->n_tx || !(p->args.outputs & (protein ? MAGOT_OUT_PEP : MAGOT_OUT_NUC))) {

@@ -787,6 +787,10 @@ struct Lowered {
   std::vector<magot_tx> txs;
   std::string text;
   std::vector<Piece> pieces;
+  // longest=True over protein candidates (genome.py:720-724): the choice
+  // depends on the peptides' trimmed lengths, so it is made at render time.
+  // Per group: the first piece of each candidate, then the group's end piece.
+  std::vector<std::vector<uint64_t>> groups;
 };
 }  // namespace magot
 
@@ -910,7 +914,7 @@ struct Lowering {
   // keeps the later candidate of a length, and the maximal key wins.  No
   // candidate: max() of an empty list, ValueError.
   uint64_t fasta_longest(const Feature& F) {
-    if (protein) throw Unsupported();  // a peptide's length depends on the genome (trimX)
+    if (protein) return fasta_longest_protein(F);
     Lowered best;
     uint64_t best_key = 0;
     bool have = false;
@@ -930,6 +934,30 @@ struct Lowering {
     }
     if (!have) throw Unsupported();
     append_lowered(P, best);
+    return 1;
+  }
+
+  // Protein: a peptide's length depends on the genome (the leading-'X' trim),
+  // so every candidate is lowered and the render picks (magot_gffplan_render).
+  uint64_t fasta_longest_protein(const Feature& F) {
+    std::vector<Lowered> cands;
+    for (uint32_t c : F.children) {
+      const int64_t o = M.lookup(c);
+      if (o < 0) throw Unsupported();
+      if (M.feats[(size_t)o].base) throw Unsupported();  // mixed children: print
+      Lowered T;
+      Lowering sub{T, M, protein, contig_idx, contig_len, id_of_feat};
+      if (sub.fasta((uint32_t)o, true) == 0) continue;  // child_fasta == ""
+      cands.push_back(std::move(T));
+    }
+    if (cands.empty()) throw Unsupported();  // max() of an empty list
+    std::vector<uint64_t> group;
+    for (const Lowered& T : cands) {
+      group.push_back(P.pieces.size());
+      append_lowered(P, T);
+    }
+    group.push_back(P.pieces.size());
+    if (cands.size() > 1) P.groups.push_back(std::move(group));
     return 1;
   }
 
@@ -1008,6 +1036,10 @@ struct Lowering {
 // Appends `part` (lowered from a later run of keys) to `all`.
 void append_lowered(Lowered& all, const Lowered& part) {
   const uint64_t x0 = all.exons.size(), t0 = all.txs.size(), c0 = all.text.size();
+  for (std::vector<uint64_t> g : part.groups) {
+    for (uint64_t& b : g) b += all.pieces.size();
+    all.groups.push_back(std::move(g));
+  }
   all.exons.insert(all.exons.end(), part.exons.begin(), part.exons.end());
   for (magot_tx t : part.txs) {
     t.exon_begin += x0;
@@ -1153,7 +1185,7 @@ bool gffplan_units(const magot_gffplan* p, const std::string** text, std::vector
   *text = &p->text;
   *protein = p->protein;
   *n_rec = p->txs.size();
-  if (p->txs.size() >= kNoRecord) return false;
+  if (p->txs.size() >= kNoRecord || !p->groups.empty()) return false;
   units->clear();
   TextUnit cur{0, 0, kNoRecord};
   for (const Piece& pc : p->pieces) {
@@ -1205,36 +1237,87 @@ int magot_gffplan_render(const magot_gffplan* p, const uint8_t* nuc, const uint6
     magot::set_error("magot_gffplan_render: null argument");
     return MAGOT_ERR_ARG;
   }
-  uint64_t total = 0;
-  for (const auto& pc : p->pieces) {
-    if (pc.rec < 0) {
-      total += pc.len;
-    } else {
+  // pieces [b, e): appended to `o` (when non-null), returns the byte count
+  auto emit = [&](uint64_t b, uint64_t e, uint8_t* o) {
+    uint64_t n = 0;
+    for (uint64_t i = b; i < e; ++i) {
+      const auto& pc = p->pieces[i];
       const uint8_t* s;
       uint64_t l;
-      payload(p, pc.rec, nuc, noff, pep, poff, &s, &l);
-      total += l;
+      if (pc.rec < 0) {
+        s = reinterpret_cast<const uint8_t*>(p->text.data()) + pc.off;
+        l = pc.len;
+      } else {
+        payload(p, pc.rec, nuc, noff, pep, poff, &s, &l);
+      }
+      if (o) memcpy(o + n, s, l);
+      n += l;
     }
-  }
+    return n;
+  };
+  // longest=True candidate key: len("".join(seq.split('\n')[1:])) of the
+  // candidate string (genome.py:722)
+  auto key = [&](uint64_t b, uint64_t e) {
+    uint64_t n = 0, first = 0;
+    bool in_first = true;
+    for (uint64_t i = b; i < e; ++i) {
+      const auto& pc = p->pieces[i];
+      if (pc.rec >= 0) {
+        const uint8_t* s;
+        uint64_t l;
+        payload(p, pc.rec, nuc, noff, pep, poff, &s, &l);
+        n += l;
+        if (in_first) first += l;
+        continue;
+      }
+      for (uint64_t k = pc.off; k < pc.off + pc.len; ++k) {
+        if (p->text[k] == '\n') {
+          in_first = false;
+          continue;
+        }
+        ++n;
+        if (in_first) ++first;
+      }
+    }
+    return n - first;
+  };
+  // the render: pieces in order, each selection group replaced by its
+  // longest candidate (the later one on a tie: a dict keyed by the length)
+  auto render = [&](uint8_t* o) {
+    uint64_t n = 0, i = 0;
+    for (const auto& g : p->groups) {
+      n += emit(i, g.front(), o ? o + n : nullptr);
+      size_t best = 0;
+      uint64_t best_key = 0;
+      for (size_t c = 0; c + 1 < g.size(); ++c) {
+        const uint64_t k = key(g[c], g[c + 1]);
+        if (c == 0 || k >= best_key) {
+          best = c;
+          best_key = k;
+        }
+      }
+      n += emit(g[best], g[best + 1], o ? o + n : nullptr);
+      i = g.back();
+    }
+    return n + emit(i, p->pieces.size(), o ? o + n : nullptr);
+  };
+  const uint64_t total = render(nullptr);
   *out_len = total;
   if (!out) return MAGOT_OK;
   if (cap < total) {
     magot::set_error("magot_gffplan_render: output buffer too small");
     return MAGOT_ERR_ARG;
   }
-  uint8_t* o = out;
-  for (const auto& pc : p->pieces) {
-    if (pc.rec < 0) {
-      memcpy(o, p->text.data() + pc.off, pc.len);
-      o += pc.len;
-    } else {
-      const uint8_t* s;
-      uint64_t l;
-      payload(p, pc.rec, nuc, noff, pep, poff, &s, &l);
-      memcpy(o, s, l);
-      o += l;
-    }
+  render(out);
+  return MAGOT_OK;
+}
+
+int magot_gffplan_selections(const magot_gffplan* p, uint64_t* n_groups) {
+  if (!p || !n_groups) {
+    magot::set_error("magot_gffplan_selections: null argument");
+    return MAGOT_ERR_ARG;
   }
+  *n_groups = p->groups.size();
   return MAGOT_OK;
 }
 

@@ -413,14 +413,20 @@ class GffPlan(object):
         self.txs = np.zeros(n_tx, dtype=TX_DTYPE)
         check(_lib.lib().magot_gffplan_tables(handle, ptr(self.exons), ptr(self.txs)),
               'magot_gffplan_tables')
+        n = ctypes.c_uint64()
+        check(_lib.lib().magot_gffplan_selections(handle, ctypes.byref(n)),
+              'magot_gffplan_selections')
+        # longest=True protein choices, made by render() from the peptides
+        # (no device text assembly for such a plan)
+        self.n_select = n.value
 
     @classmethod
     def build(cls, gff, names, lengths, feature='gene', protein=False, order='insertion',
               longest=False, genomic=False):
         """``longest`` / ``genomic``: get_fasta's options (genome.py:677-724).
         genomic=True is never translated (a nucleotide plan whatever
-        ``protein`` says); longest=True is planned for nucleotide only (None,
-        the object path, for a protein parent branch)."""
+        ``protein`` says).  longest=True over protein candidates is chosen at
+        render time (``n_select`` > 0), from the trimmed peptide lengths."""
         L = _lib.lib()
         text = _text_view(gff)
         n = len(names)

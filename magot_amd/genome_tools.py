@@ -66,9 +66,8 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
 
     The native planner (magot_gff_plan: read_gff + get_fasta lowering in C++)
     and one kernel launch serve the default call, genomic=True and
-    longest=True; inputs that take one of the reference's diagnostic paths,
-    longest protein parents (a peptide's length depends on the genome) and
-    from_exons use the object path (``native=False`` forces it)."""
+    longest=True; inputs that take one of the reference's diagnostic paths
+    and from_exons use the object path (``native=False`` forces it)."""
     lg, gm = _literal(longest), _literal(genomic)
     if (native == 'True' and from_exons != 'True' and isinstance(lg, bool) and
             isinstance(gm, bool) and seq_type in ('nucleotide', 'protein')):
@@ -109,6 +108,13 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
     try:
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                    engine.OUT_PEP if plan.protein else engine.OUT_NUC)
+        if plan.n_select:
+            # longest=True over peptides: the render picks from the trimmed
+            # lengths, on the host
+            try:
+                return plan.render(*ex.run())
+            finally:
+                ex.close()
         text = engine.FastaText(plan, ex)
         try:
             ex.execute()

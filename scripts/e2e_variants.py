@@ -1,4 +1,4 @@
-"""Times gff2fasta's longest=True and genomic=True variants on the native path
+"""Times gff2fasta's longest=True (nucleotide and protein) and genomic=True variants on the native path
 over the files of an e2e_cli.py run (C3 by default), each in this process
 after one warm call of the default variant (device start-up excluded).
 Correctness of these variants is pinned by tests/test_gffplan.py (oracle) and
@@ -25,10 +25,12 @@ def main():
     fa, gf = os.path.join(a.dir, 'genome.fa'), os.path.join(a.dir, 'ann.gff3')
     genome_tools._gff2fasta_native(fa, gf, 'nucleotide', 'py2')  # warm: device start-up
     rec = {}
-    for name, kw in (('default_nucleotide', {}), ('longest_nucleotide', {'longest': True}),
-                     ('genomic', {'genomic': True})):
+    for name, st, kw in (('default_nucleotide', 'nucleotide', {}),
+                         ('longest_nucleotide', 'nucleotide', {'longest': True}),
+                         ('longest_protein', 'protein', {'longest': True}),
+                         ('genomic', 'nucleotide', {'genomic': True})):
         t = time.perf_counter()
-        text = genome_tools._gff2fasta_native(fa, gf, 'nucleotide', 'py2', **kw)
+        text = genome_tools._gff2fasta_native(fa, gf, st, 'py2', **kw)
         rec[name] = {'s': time.perf_counter() - t, 'native': text is not None,
                      'bytes': None if text is None else int(len(text)) + 1}
     print(json.dumps(rec), flush=True)

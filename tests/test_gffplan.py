@@ -244,8 +244,8 @@ def _oracle_or_diag(fasta, gff, **kw):
 @pytest.mark.parametrize('i', range(len(FUZZ_INPUTS)))
 def test_native_longest_and_genomic_match_oracle(i):
     fasta, gff = FUZZ_INPUTS[i]
-    calls = [dict(seq_type='nucleotide', longest=True), dict(seq_type='nucleotide', genomic=True),
-             dict(seq_type='protein', genomic=True),
+    calls = [dict(seq_type='nucleotide', longest=True), dict(seq_type='protein', longest=True),
+             dict(seq_type='nucleotide', genomic=True), dict(seq_type='protein', genomic=True),
              dict(seq_type='protein', genomic=True, longest=True)]
     for kw in calls:
         for order in ('insertion', 'py2'):
@@ -295,9 +295,12 @@ def test_native_longest_synthetic():
                             % (a, b, st, g, m, g, m))
     gff = '\n'.join(rows) + '\n'
     for order in ('py2', 'insertion'):
-        got = native_gff2fasta(fasta, gff, 'nucleotide', order, longest=True)
-        assert got is not None
-        assert got == mo.gff2fasta(fasta, gff, seq_type='nucleotide', order=order, longest=True)
+        for seq_type in ('nucleotide', 'protein'):
+            got = native_gff2fasta(fasta, gff, seq_type, order, longest=True)
+            want, diag = _oracle_or_diag(fasta, gff, seq_type=seq_type, order=order, longest=True)
+            assert (got is None) == diag, seq_type  # protein: records below one codon
+            if got is not None:
+                assert got == want, seq_type
         gen = native_gff2fasta(fasta, gff.replace('\tID=g7\n', '\tID=g7\n'), 'protein', order,
                                genomic=True)
         want, diag = _oracle_or_diag(fasta, gff, seq_type='protein', order=order, genomic=True)
@@ -306,10 +309,23 @@ def test_native_longest_synthetic():
             assert gen == want
 
 
-def test_native_longest_protein_declines():
-    gs = G.GenomeSequence('>c1\nATGAAACCCGGGTTTTAA\n')
-    gff = ('c1\tx\tgene\t1\t18\t.\t+\t.\tID=g1\n'
-           'c1\tx\tmRNA\t1\t18\t.\t+\t.\tID=m1;Parent=g1\n'
-           'c1\tx\tCDS\t1\t18\t.\t+\t0\tID=c1;Parent=m1\n')
-    assert engine.GffPlan.build(gff, list(gs), [18], protein=True, longest=True) is None
-    assert engine.GffPlan.build(gff, list(gs), [18], protein=False, longest=True) is not None
+def test_native_longest_protein_picks_by_trimmed_length():
+    """Two transcripts whose CDS are 12 bases each: four codons, but the
+    first one's leading codon holds an N, so trimX drops its 'X' and the
+    second (4 residues against 3) is the longest; swapped, the later one
+    wins the tie (genome.py:720-724)."""
+    seq = 'NAAATGGCCTTT' + 'ATGAAACCCGGG'
+    fasta = '>c1\n' + seq + '\n'
+    head = 'c1\tx\tgene\t1\t24\t.\t+\t.\tID=g1\n'
+    def tx(name, a, b):
+        return ('c1\tx\tmRNA\t%d\t%d\t.\t+\t.\tID=%s;Parent=g1\n' % (a, b, name) +
+                'c1\tx\tCDS\t%d\t%d\t.\t+\t0\tID=%s.c;Parent=%s\n' % (a, b, name, name))
+    for gff in (head + tx('m1', 1, 12) + tx('m2', 13, 24), head + tx('m2', 13, 24) + tx('m1', 1, 12),
+                head + tx('m1', 13, 24) + tx('m2', 13, 24)):
+        gs = G.GenomeSequence(fasta)
+        plan = engine.GffPlan.build(gff, list(gs), [24], protein=True, longest=True)
+        assert plan is not None and plan.n_select == 1
+        plan.close()
+        for order in ('insertion', 'py2'):
+            got = native_gff2fasta(fasta, gff, 'protein', order, longest=True)
+            assert got == mo.gff2fasta(fasta, gff, seq_type='protein', order=order, longest=True)
