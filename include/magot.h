@@ -269,7 +269,10 @@ void magot_orf6_destroy(magot_orf6* o);
  * sequence, the later one on a tie).  For protein the lengths depend on the
  * leading-'X' trim, i.e. on the genome: every candidate is planned and
  * magot_gffplan_render picks (magot_gffplan_selections > 0; such a plan has
- * no device text assembly).
+ * no device text assembly).  MAGOT_GFF_FROM_EXONS: gff2fasta's
+ * from_exons="True" reading (genome_tools.py:326-327: "\texon\t" replaced by
+ * "\tCDS\t" in each line, then every type that is a substring of "CDS"
+ * ignored).
  * Returns MAGOT_ERR_UNSUPPORTED when the input would take one of the
  * reference's diagnostic paths (prints, None, exceptions): the caller then
  * uses the object path, which reproduces them.
@@ -278,6 +281,7 @@ void magot_orf6_destroy(magot_orf6* o);
 #define MAGOT_GFF_ORDER_PY2 2u
 #define MAGOT_GFF_LONGEST 4u
 #define MAGOT_GFF_GENOMIC 8u
+#define MAGOT_GFF_FROM_EXONS 16u
 typedef struct magot_gffplan magot_gffplan;
 int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
                    const uint64_t* contig_lens, uint32_t n_contigs, const char* feature,

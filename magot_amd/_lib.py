@@ -47,6 +47,7 @@ GFF_PROTEIN = 1
 GFF_ORDER_PY2 = 2
 GFF_LONGEST = 4
 GFF_GENOMIC = 8
+GFF_FROM_EXONS = 16
 
 
 class MagotError(RuntimeError):

@@ -331,6 +331,10 @@ struct Arena {
 // Settings read_gff fixes on the first accepted line (genome.py:262-292).
 struct GffFormat {
   int version = 0;  // 0 = auto (no accepted line yet)
+  // gff2fasta(from_exons="True") (genome_tools.py:326-327): features_to_replace
+  // [('exon', 'CDS')] and features_to_ignore="CDS", a str, so `in` is a
+  // substring test
+  bool from_exons = false;
   bool have_id_field = true, have_parent_field = true;  // IDfield='ID', parent_field='Parent'
   std::vector<std::string> hierarchy;
 };
@@ -448,11 +452,30 @@ struct LineParser {
 
   // false: the line is skipped; throws Unsupported on a diagnostic path
   bool parse(const char* raw, uint64_t rl, GffLine& L) {
+    if (F.from_exons && sv(raw, rl).find("\texon\t") != sv::npos) {
+      // line.replace("\texon\t", "\tCDS\t") (genome.py:285-286): left to right,
+      // non-overlapping; the tab count (checked before, :283) is unchanged
+      // (into the arena: the parsed line's views must outlive this call)
+      const sv line(raw, rl);
+      char* o = arena.alloc(rl);
+      size_t m = 0, b = 0;
+      for (size_t e; (e = line.find("\texon\t", b)) != sv::npos; b = e + 6) {
+        memcpy(o + m, line.data() + b, e - b);
+        m += e - b;
+        memcpy(o + m, "\tCDS\t", 5);
+        m += 5;
+      }
+      memcpy(o + m, line.data() + b, rl - b);
+      m += rl - b;
+      raw = o;
+      rl = m;
+    }
     sv cols[9];
     if (!split_line(raw, rl, arena, cols)) return false;
     const sv tags_text = cols[8];
     const sv ftype = cols[2];
-    if (ftype == "exon") return false;  // features_to_ignore default
+    // features_to_ignore: ['exon'] by default; "CDS" (substring test) for from_exons
+    if (F.from_exons ? sv("CDS").find(ftype) != sv::npos : ftype == "exon") return false;
     int64_t lo = parse_int(cols[3]), hi = parse_int(cols[4]);
     if (lo > hi) std::swap(lo, hi);
     L.lo = lo;
@@ -528,9 +551,10 @@ struct LineParser {
 // parallel over newline-aligned chunks of the text, then the model updates
 // (de-duplication, tables, parents) in file order.  Any diagnostic path
 // anywhere declines the whole input, so chunks may find them out of order.
-void read_gff(Model& M, const char* text, uint64_t n) {
+void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
   const auto t_start = std::chrono::steady_clock::now();
   GffFormat F;
+  F.from_exons = from_exons;
   {  // the first accepted line fixes the format
     Arena arena;
     sv cols[9];
@@ -1082,7 +1106,7 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
     t0 = t1;
   };
   try {
-    magot::read_gff(P->model, gff, gff_len);
+    magot::read_gff(P->model, gff, gff_len, (flags & MAGOT_GFF_FROM_EXONS) != 0);
     lap("read_gff");
     magot::Model& M = P->model;
     std::unordered_map<std::string, uint32_t> contig_of;

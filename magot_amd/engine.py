@@ -422,7 +422,7 @@ class GffPlan(object):
 
     @classmethod
     def build(cls, gff, names, lengths, feature='gene', protein=False, order='insertion',
-              longest=False, genomic=False):
+              longest=False, genomic=False, from_exons=False):
         """``longest`` / ``genomic``: get_fasta's options (genome.py:677-724).
         genomic=True is never translated (a nucleotide plan whatever
         ``protein`` says).  longest=True over protein candidates is chosen at
@@ -434,7 +434,8 @@ class GffPlan(object):
         lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
         flags = (_lib.GFF_PROTEIN if protein else 0) | \
             (_lib.GFF_ORDER_PY2 if order == 'py2' else 0) | \
-            (_lib.GFF_LONGEST if longest else 0) | (_lib.GFF_GENOMIC if genomic else 0)
+            (_lib.GFF_LONGEST if longest else 0) | (_lib.GFF_GENOMIC if genomic else 0) | \
+            (_lib.GFF_FROM_EXONS if from_exons else 0)
         h = ctypes.c_void_p()
         ne, nt = ctypes.c_uint64(), ctypes.c_uint64()
         rc = L.magot_gff_plan(_text_ptr(text), len(text), arr, lens.ctypes.data_as(_lib._u64p), n,

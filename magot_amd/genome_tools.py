@@ -65,14 +65,14 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
     """genome_tools.py:324-330.
 
     The native planner (magot_gff_plan: read_gff + get_fasta lowering in C++)
-    and one kernel launch serve the default call, genomic=True and
-    longest=True; inputs that take one of the reference's diagnostic paths
-    and from_exons use the object path (``native=False`` forces it)."""
+    and one kernel launch serve every combination of from_exons, genomic and
+    longest; inputs that take one of the reference's diagnostic paths use the
+    object path (``native=False`` forces it)."""
     lg, gm = _literal(longest), _literal(genomic)
-    if (native == 'True' and from_exons != 'True' and isinstance(lg, bool) and
-            isinstance(gm, bool) and seq_type in ('nucleotide', 'protein')):
+    if (native == 'True' and isinstance(lg, bool) and isinstance(gm, bool) and
+            seq_type in ('nucleotide', 'protein')):
         text = _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=lg is True,
-                                 genomic=gm is True)
+                                 genomic=gm is True, from_exons=from_exons == 'True')
         if text is not None:
             _write_bytes(text, b'\n')
             return
@@ -87,7 +87,8 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
     _write(text + '\n')
 
 
-def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, genomic=False):
+def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, genomic=False,
+                      from_exons=False):
     """The gff2fasta text (bytes) via the native planner, the extraction
     kernel and device text assembly, or None when the planner declines."""
     if order not in ('py2', 'insertion'):
@@ -102,7 +103,8 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
     names = dev.names
     protein = seq_type == 'protein'
     plan = engine.GffPlan.build(genome.read_buffer(gff), names, [int(x) for x in dev.lengths],
-                                protein=protein, order=order, longest=longest, genomic=genomic)
+                                protein=protein, order=order, longest=longest, genomic=genomic,
+                                from_exons=from_exons)
     if plan is None:
         return None
     try:

@@ -42,12 +42,12 @@ def _payloads(plan, seqs):
 
 
 def native_gff2fasta(fasta, gff, seq_type='nucleotide', order='insertion', longest=False,
-                     genomic=False):
+                     genomic=False, from_exons=False):
     gs = G.GenomeSequence(fasta)
     names = list(gs)
     plan = engine.GffPlan.build(G.ensure_file(gff).read(), names, [len(gs[n]) for n in names],
                                 protein=seq_type == 'protein', order=order, longest=longest,
-                                genomic=genomic)
+                                genomic=genomic, from_exons=from_exons)
     if plan is None:
         return None
     text = plan.render(*_payloads(plan, [gs[n] for n in names]))
@@ -246,7 +246,9 @@ def test_native_longest_and_genomic_match_oracle(i):
     fasta, gff = FUZZ_INPUTS[i]
     calls = [dict(seq_type='nucleotide', longest=True), dict(seq_type='protein', longest=True),
              dict(seq_type='nucleotide', genomic=True), dict(seq_type='protein', genomic=True),
-             dict(seq_type='protein', genomic=True, longest=True)]
+             dict(seq_type='protein', genomic=True, longest=True),
+             dict(seq_type='nucleotide', from_exons=True), dict(seq_type='protein', from_exons=True),
+             dict(seq_type='nucleotide', from_exons=True, genomic=True)]
     for kw in calls:
         for order in ('insertion', 'py2'):
             got = native_gff2fasta(fasta, gff, order=order, **kw)
@@ -329,3 +331,31 @@ def test_native_longest_protein_picks_by_trimmed_length():
         for order in ('insertion', 'py2'):
             got = native_gff2fasta(fasta, gff, 'protein', order, longest=True)
             assert got == mo.gff2fasta(fasta, gff, seq_type='protein', order=order, longest=True)
+
+
+def test_native_from_exons_replace_and_substring_ignore():
+    """from_exons="True" (genome_tools.py:326-327): "\texon\t" becomes "\tCDS\t"
+    anywhere in the line (the source column too, non-overlapping, left to
+    right), then every type that is a substring of "CDS" ("", C, D, S, CD,
+    DS, CDS) is ignored; other types stay (genomic spans over what remains)."""
+    fasta = '>c1\n' + 'ACGTTGCA' * 40 + '\n'
+    rows = ['c1\tx\tgene\t1\t300\t.\t+\t.\tID=g1',
+            'c1\texon\tmRNA\t5\t200\t.\t+\t.\tID=m1;Parent=g1',
+            'c1\tx\texon\t5\t50\t.\t+\t.\tID=e1;Parent=m1',
+            'c1\tx\tCD\t60\t70\t.\t+\t.\tID=x1;Parent=m1',
+            'c1\tx\tregion\t80\t90\t.\t+\t.\tID=r1;Parent=m1',
+            'c1\tx\tgene\t100\t250\t.\t-\t.\tID=g2',
+            'c1\texon\tmRNA\t100\t250\t.\t-\t.\tID=m2;Parent=g2',
+            'c1\tx\tUTR\t100\t120\t.\t-\t.\tID=u2;Parent=m2']
+    gff = '\n'.join(rows) + '\n'
+    planned = 0
+    for kw in (dict(), dict(genomic=True), dict(longest=True)):
+        for seq_type in ('nucleotide', 'protein'):
+            got = native_gff2fasta(fasta, gff, seq_type, 'insertion', from_exons=True, **kw)
+            want, diag = _oracle_or_diag(fasta, gff, seq_type=seq_type, order='insertion',
+                                         from_exons=True, **kw)
+            assert (got is None) == diag, (kw, seq_type)
+            if got is not None:
+                assert got == want, (kw, seq_type)
+                planned += 1
+    assert planned >= 2  # genomic and longest hit the reference's TypeError / ValueError on g2
