@@ -1,4 +1,5 @@
-"""Times gff2fasta's longest=True (nucleotide and protein) and genomic=True variants on the native path
+"""Times gff2fasta's longest=True (nucleotide and protein) and genomic=True variants,
+and cds2pep over the nucleotide output, on the native path
 over the files of an e2e_cli.py run (C3 by default), each in this process
 after one warm call of the default variant (device start-up excluded).
 Correctness of these variants is pinned by tests/test_gffplan.py (oracle) and
@@ -33,6 +34,20 @@ def main():
         text = genome_tools._gff2fasta_native(fa, gf, st, 'py2', **kw)
         rec[name] = {'s': time.perf_counter() - t, 'native': text is not None,
                      'bytes': None if text is None else int(len(text)) + 1}
+        if name == 'default_nucleotide':  # the CDS FASTA cds2pep reads below
+            with open(os.path.join(a.dir, 'cds.fa'), 'wb') as fh:
+                fh.write(bytes(text))
+                fh.write(b'\n')
+    # cds2pep (genome_tools.py:664-675) on that CDS FASTA (500k records)
+    import io
+    from contextlib import redirect_stdout
+    b = io.BytesIO()
+    w = io.TextIOWrapper(b, encoding='latin-1', write_through=True)
+    t = time.perf_counter()
+    with redirect_stdout(w):
+        genome_tools.cds2pep(os.path.join(a.dir, 'cds.fa'))
+    w.flush()
+    rec['cds2pep'] = {'s': time.perf_counter() - t, 'bytes': len(b.getvalue())}
     print(json.dumps(rec), flush=True)
 
 
