@@ -127,6 +127,29 @@ int magot_fasta_read(const char* text, uint64_t len, int truncate_names, uint32_
                      uint64_t* lens, char* names, uint64_t names_cap, uint64_t* names_len,
                      uint8_t* seqs, uint64_t seqs_cap);
 
+/*
+ * cds2pep (genome_tools.py:664-675) without a per-line loop.  magot_cds_scan
+ * splits `text` into lines ('\n'; a CR before it is dropped): lines starting
+ * with '>' are headers (hdr_off / hdr_len[n_seg-1]), all others are appended
+ * to the current sequence; segment k (seq[seg_off[k]:seg_off[k+1]], n_seg+1
+ * offsets) is the sequence before header k, the last one follows the last
+ * header.  Call with NULL buffers for n_seg / seq_bytes first.
+ * MAGOT_ERR_UNSUPPORTED: an empty line (the reference's IndexError) or a CR
+ * inside a line; the caller's line loop reproduces both.  magot_cds_render
+ * writes the tool's stdout from the frame-0 translations of the segments
+ * (magot_translate_batch layout: poff, codons < 0 for None): a translation
+ * for every non-empty segment before a header and for the last one ("None"
+ * when translate() returns None, one leading 'X' trimmed), each header after
+ * its segment.  out == NULL: *out_len only.
+ */
+int magot_cds_scan(const char* text, uint64_t len, uint64_t* n_seg, uint64_t* seq_bytes,
+                   uint64_t* seg_off, uint64_t* hdr_off, uint64_t* hdr_len, uint8_t* seq,
+                   uint64_t seq_cap);
+int magot_cds_render(const char* text, uint64_t n_seg, const uint64_t* seg_off,
+                     const uint64_t* hdr_off, const uint64_t* hdr_len, const uint8_t* pep,
+                     const uint64_t* poff, const int64_t* codons, uint8_t* out, uint64_t cap,
+                     uint64_t* out_len);
+
 /* Sizes of a loaded genome: total bases, exception runs, device bytes held. */
 int magot_genome_stats(const magot_genome* g, uint64_t* total_bases, uint64_t* n_exc_runs,
                        uint64_t* device_bytes);

@@ -32,7 +32,7 @@ EXPORTS = (
     'magot_plan_algorithmic_bytes',
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
     'magot_gff_plan', 'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
-    'magot_gffplan_selections',
+    'magot_gffplan_selections', 'magot_cds_scan', 'magot_cds_render',
     'magot_genome_export', 'magot_genome_copy_arena', 'magot_genome_attach',
     'magot_plan_copy_outputs',
     'magot_orf6_sizes', 'magot_orf6_batch', 'magot_plan_orf6', 'magot_orf6_execute',
@@ -102,6 +102,10 @@ def _declare(lib):
                                                 _u64p]),
         'magot_gffplan_destroy': (None, [_vp]),
         'magot_gffplan_selections': (ctypes.c_int, [_vp, _u64p]),
+        'magot_cds_scan': (ctypes.c_int, [_vp, ctypes.c_uint64, _u64p, _u64p, _vp, _vp, _vp, _vp,
+                                          ctypes.c_uint64]),
+        'magot_cds_render': (ctypes.c_int, [_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _vp, ctypes.c_uint64, _u64p]),
         'magot_genome_export': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _u64p, _u64p]),
         'magot_genome_copy_arena': (ctypes.c_int, [_vp, _vp]),
         'magot_genome_attach': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp,

@@ -264,3 +264,95 @@ extern "C" int magot_fasta_read(const char* text, uint64_t len, int truncate_nam
   if (seqs) magot::parallel_for(k, [&](size_t i) { magot::copy_contig(fc.src[i], seqs + at[i]); });
   return MAGOT_OK;
 }
+
+// ---------------------------------------------------------------------------
+// cds2pep (genome_tools.py:664-675): the file's lines with '\n' and '\r'
+// removed; a line starting with '>' is echoed and ends the sequence gathered
+// so far (translated if non-empty), every other line is appended to it, and
+// the last sequence is translated whatever its length.
+// ---------------------------------------------------------------------------
+
+extern "C" int magot_cds_scan(const char* text, uint64_t len, uint64_t* n_seg,
+                              uint64_t* seq_bytes, uint64_t* seg_off, uint64_t* hdr_off,
+                              uint64_t* hdr_len, uint8_t* seq, uint64_t seq_cap) {
+  if (!n_seg || !seq_bytes || (len && !text)) {
+    magot::set_error("magot_cds_scan: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  uint64_t k = 0, m = 0;  // headers seen, sequence bytes
+  if (seg_off) seg_off[0] = 0;
+  for (uint64_t pos = 0; pos < len;) {
+    const char* nl = static_cast<const char*>(memchr(text + pos, '\n', len - pos));
+    const uint64_t end = nl ? (uint64_t)(nl - text) : len;
+    uint64_t e = end;
+    if (e > pos && text[e - 1] == '\r') --e;  // CRLF
+    if (e == pos) {  // empty after the strip: line[0] raises IndexError
+      magot::set_error("magot_cds_scan: empty line (the line loop reproduces the IndexError)");
+      return MAGOT_ERR_UNSUPPORTED;
+    }
+    if (memchr(text + pos, '\r', e - pos)) {  // a CR inside the line: the line loop strips it
+      magot::set_error("magot_cds_scan: carriage return inside a line");
+      return MAGOT_ERR_UNSUPPORTED;
+    }
+    if (text[pos] == '>') {
+      if (hdr_off) {
+        hdr_off[k] = pos;
+        hdr_len[k] = e - pos;
+      }
+      ++k;
+      if (seg_off) seg_off[k] = m;
+    } else {
+      if (seq) {
+        if (m + (e - pos) > seq_cap) {
+          magot::set_error("magot_cds_scan: buffer too small");
+          return MAGOT_ERR_ARG;
+        }
+        memcpy(seq + m, text + pos, e - pos);
+      }
+      m += e - pos;
+    }
+    pos = nl ? end + 1 : len;
+  }
+  *n_seg = k + 1;
+  *seq_bytes = m;
+  if (seg_off) seg_off[k + 1] = m;
+  return MAGOT_OK;
+}
+
+extern "C" int magot_cds_render(const char* text, uint64_t n_seg, const uint64_t* seg_off,
+                                const uint64_t* hdr_off, const uint64_t* hdr_len,
+                                const uint8_t* pep, const uint64_t* poff, const int64_t* codons,
+                                uint8_t* out, uint64_t cap, uint64_t* out_len) {
+  if (!out_len || !n_seg || !seg_off || !poff || !codons || (n_seg > 1 && (!text || !hdr_off || !hdr_len))) {
+    magot::set_error("magot_cds_render: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  uint64_t n = 0;
+  auto put = [&](const void* s, uint64_t l) {
+    if (out && n + l <= cap) memcpy(out + n, s, l);
+    n += l;
+  };
+  for (uint64_t k = 0; k < n_seg; ++k) {
+    if (k == n_seg - 1 || seg_off[k + 1] > seg_off[k]) {
+      if (codons[k] < 0) {
+        put("None", 4);  // translate() returned None (genome.py:810)
+      } else {
+        uint64_t a = poff[k];
+        const uint64_t b = poff[k + 1];
+        if (b > a && pep[a] == 'X') ++a;  // trimX (genome.py:819-821)
+        put(pep + a, b - a);
+      }
+      put("\n", 1);
+    }
+    if (k + 1 < n_seg) {
+      put(text + hdr_off[k], hdr_len[k]);
+      put("\n", 1);
+    }
+  }
+  *out_len = n;
+  if (out && n > cap) {
+    magot::set_error("magot_cds_render: buffer too small");
+    return MAGOT_ERR_ARG;
+  }
+  return MAGOT_OK;
+}

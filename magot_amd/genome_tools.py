@@ -24,6 +24,7 @@ Python-3 order.
 """
 
 import ast
+import ctypes
 import sys
 
 import numpy as np
@@ -129,12 +130,72 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
         plan.close()
 
 
-def cds2pep(fasta_file):
+def _cds_translate(seq, seg_off):
+    """(pep offsets, codon counts, residues) of the segments' frame-0 '+'
+    translations (magot_translate_batch, one launch)."""
+    from . import _lib
+    n = len(seg_off) - 1
+    fr = np.zeros(n, np.int32)
+    st = np.full(n, ord('+'), np.uint8)
+    poff = np.empty(n + 1, dtype=np.uint64)
+    codons = np.empty(max(n, 1), dtype=np.int64)
+    L = _lib.lib()
+    _lib.check(L.magot_translate_sizes(_lib.ptr(seg_off), n, _lib.ptr(fr), _lib.ptr(poff),
+                                       _lib.ptr(codons)), 'magot_translate_sizes')
+    out = np.empty(max(int(poff[n]), 1), dtype=np.uint8)
+    _lib.check(L.magot_translate_batch(_lib.default_context().handle,
+                                       _lib.ptr(seq) if len(seq) else None, _lib.ptr(seg_off), n,
+                                       _lib.ptr(fr), _lib.ptr(st), None, _lib.ptr(poff),
+                                       _lib.ptr(out)), 'magot_translate_batch')
+    return poff, codons, out
+
+
+def _cds2pep_native(data):
+    """cds2pep's stdout for a file's bytes: magot_cds_scan (no per-line
+    Python), one translation batch, magot_cds_render; None when the line loop
+    must run (an empty line's IndexError, a CR inside a line)."""
+    from . import _lib
+    L = _lib.lib()
+    d = engine._text_view(data)
+    tp = engine._text_ptr(d)
+    n_seg, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = L.magot_cds_scan(tp, len(d), ctypes.byref(n_seg), ctypes.byref(nb), None, None, None,
+                          None, 0)
+    if rc == _lib.ERR_UNSUPPORTED:
+        return None
+    _lib.check(rc, 'magot_cds_scan')
+    n = n_seg.value
+    seg_off = np.empty(n + 1, np.uint64)
+    hdr_off = np.empty(max(n - 1, 1), np.uint64)
+    hdr_len = np.empty(max(n - 1, 1), np.uint64)
+    seq = np.empty(max(nb.value, 1), np.uint8)
+    _lib.check(L.magot_cds_scan(tp, len(d), ctypes.byref(n_seg), ctypes.byref(nb),
+                                _lib.ptr(seg_off), _lib.ptr(hdr_off), _lib.ptr(hdr_len),
+                                _lib.ptr(seq), len(seq)), 'magot_cds_scan')
+    poff, codons, pep = _cds_translate(seq[:nb.value], seg_off)
+    size = ctypes.c_uint64()
+    args = (tp, n, _lib.ptr(seg_off), _lib.ptr(hdr_off), _lib.ptr(hdr_len), _lib.ptr(pep),
+            _lib.ptr(poff), _lib.ptr(codons))
+    _lib.check(L.magot_cds_render(*args, None, 0, ctypes.byref(size)), 'magot_cds_render')
+    out = np.empty(max(size.value, 1), np.uint8)
+    _lib.check(L.magot_cds_render(*args, _lib.ptr(out), size.value, ctypes.byref(size)),
+               'magot_cds_render')
+    return out[:size.value]
+
+
+def cds2pep(fasta_file, native='True'):
     """genome_tools.py:664-675: headers echoed, each record translated; all
-    records go to the GPU as one batch."""
+    records go to the GPU as one batch.  A file path is scanned natively
+    (``native=False`` forces the line loop, which also reproduces the
+    reference's IndexError on an empty line)."""
     if not hasattr(fasta_file, 'read'):
         with open(fasta_file, 'rb'):  # the reference open()s the path (:666): a missing file raises
             pass
+        if native == 'True' and isinstance(fasta_file, str):
+            text = _cds2pep_native(genome.read_buffer(fasta_file))
+            if text is not None:
+                _write_bytes(text)
+                return
     events = []       # ('line', text) | ('pep', job index)
     seqs = []
     failure = None

@@ -41,13 +41,18 @@ def main():
     # cds2pep (genome_tools.py:664-675) on that CDS FASTA (500k records)
     import io
     from contextlib import redirect_stdout
-    b = io.BytesIO()
-    w = io.TextIOWrapper(b, encoding='latin-1', write_through=True)
-    t = time.perf_counter()
-    with redirect_stdout(w):
-        genome_tools.cds2pep(os.path.join(a.dir, 'cds.fa'))
-    w.flush()
-    rec['cds2pep'] = {'s': time.perf_counter() - t, 'bytes': len(b.getvalue())}
+    outs = {}
+    for native in ('True', 'False'):
+        b = io.BytesIO()
+        w = io.TextIOWrapper(b, encoding='latin-1', write_through=True)
+        t = time.perf_counter()
+        with redirect_stdout(w):
+            genome_tools.cds2pep(os.path.join(a.dir, 'cds.fa'), native=native)
+        w.flush()
+        rec['cds2pep_' + ('native' if native == 'True' else 'line_loop')] = {
+            's': time.perf_counter() - t, 'bytes': len(b.getvalue())}
+        outs[native] = b.getvalue()
+    rec['cds2pep_outputs_equal'] = outs['True'] == outs['False']
     print(json.dumps(rec), flush=True)
 
 

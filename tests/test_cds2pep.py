@@ -70,3 +70,61 @@ def test_gpu_cds2pep_matches_reference(tmp_path, i):
     text, exc = _run(genome_tools.cds2pep, path)
     assert exc == CASES[i]['exc']
     assert text == CASES[i]['stdout']
+
+
+def _oracle_translate(seq, seg_off):
+    """Stand-in for the GPU batch in the CPU tests of the native scan and
+    render: the oracle's untrimmed frame-0 translations, in
+    magot_translate_batch layout."""
+    import numpy as np
+    s = bytes(seq).decode('latin-1')
+    n = len(seg_off) - 1
+    peps, codons = [], []
+    for k in range(n):
+        p = mo.translate(s[int(seg_off[k]):int(seg_off[k + 1])], trimX=False)
+        codons.append(-1 if p is None else len(p))
+        peps.append(p or '')
+    poff = np.zeros(n + 1, np.uint64)
+    poff[1:] = np.cumsum([len(p) for p in peps])
+    out = np.frombuffer((''.join(peps) + ' ').encode('latin-1'), np.uint8).copy()
+    return poff, np.array(codons, np.int64), out
+
+
+@pytest.mark.parametrize('i', range(len(CASES)))
+def test_native_scan_matches_reference(monkeypatch, i):
+    """magot_cds_scan + magot_cds_render (host), with the translation batch
+    replaced by the oracle: the reference's stdout, or a decline where the
+    reference raises IndexError on an empty line (the line loop then runs)."""
+    from magot_amd import genome_tools
+    monkeypatch.setattr(genome_tools, '_cds_translate', _oracle_translate)
+    got = genome_tools._cds2pep_native(CASES[i]['fasta'].encode('ascii'))
+    if got is None:
+        assert CASES[i]['exc'] == 'IndexError'
+        return
+    assert CASES[i]['exc'] is None
+    assert got.tobytes().decode('latin-1') == CASES[i]['stdout']
+
+
+@pytest.mark.parametrize('eol', ['\n', '\r\n'])
+@pytest.mark.parametrize('final_eol', [True, False])
+def test_native_scan_wrapped_records(monkeypatch, tmp_path, eol, final_eol):
+    """300 records of 0-400 bases in 60-base lines (empty records, records
+    below one codon), CRLF or LF, with or without a final newline, and a
+    sequence before the first header; an empty file prints None."""
+    import numpy as np
+    from magot_amd import genome_tools
+    monkeypatch.setattr(genome_tools, '_cds_translate', _oracle_translate)
+    rng = np.random.default_rng(5)
+    lines = ['ACGTTT']
+    for r in range(300):
+        lines.append('>rec%d some description' % r)
+        seq = ''.join(rng.choice(list('ACGTacgtNRY*'), int(rng.integers(0, 400))))
+        for a in range(0, len(seq), 60):
+            lines.append(seq[a:a + 60])
+    for text in (eol.join(lines) + (eol if final_eol else ''), ''):
+        path = tmp_path / 'cds.fa'
+        path.write_bytes(text.encode('latin-1'))
+        out = io.StringIO()
+        mo.cds2pep(str(path), out=out)
+        got = genome_tools._cds2pep_native(text.encode('latin-1'))
+        assert got.tobytes().decode('latin-1') == out.getvalue()
