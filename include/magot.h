@@ -209,6 +209,11 @@ int magot_run(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off
  * HIP events around each launch; *avg_ms receives the mean launch duration.
  */
 int magot_plan_time(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms);
+/* The same with ONE event pair around `iters` back-to-back launches: the
+ * per-launch time of a step loop, the figure bench.py's roofline uses (it
+ * agrees with rocprofv3's kernel-trace average; an isolated launch also pays
+ * the launch latency, which dominates small plans such as C2). */
+int magot_plan_time_b2b(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms);
 
 /* D2D copy of a plan's outputs (nuc_bytes / pep_bytes) into caller device
  * memory, e.g. the buffers an output gather sends. */
@@ -271,6 +276,7 @@ int magot_orf6_execute(magot_ctx* ctx, magot_orf6* o);
 int magot_orf6_fetch(magot_ctx* ctx, magot_orf6* o, uint8_t* out, uint64_t* stream_off,
                      uint64_t* stream_len);
 int magot_orf6_time(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms);
+int magot_orf6_time_b2b(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms);
 void magot_orf6_destroy(magot_orf6* o);
 
 /*

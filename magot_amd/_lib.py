@@ -28,7 +28,7 @@ EXPORTS = (
     'magot_ctx_create', 'magot_ctx_destroy', 'magot_ctx_sync', 'magot_ctx_info',
     'magot_genome_load', 'magot_genome_stats', 'magot_genome_destroy',
     'magot_plan_create', 'magot_plan_destroy', 'magot_plan_execute', 'magot_plan_fetch',
-    'magot_run', 'magot_plan_time', 'magot_plan_device_outputs',
+    'magot_run', 'magot_plan_time', 'magot_plan_time_b2b', 'magot_plan_device_outputs',
     'magot_plan_algorithmic_bytes',
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
     'magot_gff_plan', 'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
@@ -36,7 +36,7 @@ EXPORTS = (
     'magot_genome_export', 'magot_genome_copy_arena', 'magot_genome_attach',
     'magot_plan_copy_outputs',
     'magot_orf6_sizes', 'magot_orf6_batch', 'magot_plan_orf6', 'magot_orf6_execute',
-    'magot_orf6_fetch', 'magot_orf6_time', 'magot_orf6_destroy',
+    'magot_orf6_fetch', 'magot_orf6_time', 'magot_orf6_time_b2b', 'magot_orf6_destroy',
     'magot_genome_load_fasta', 'magot_genome_contigs', 'magot_fasta_read',
     'magot_fasta_text_create', 'magot_fasta_text_execute', 'magot_fasta_text_fetch',
     'magot_fasta_text_time', 'magot_fasta_text_destroy',
@@ -86,6 +86,8 @@ def _declare(lib):
         'magot_run': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
         'magot_plan_time': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_double)]),
+        'magot_plan_time_b2b': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_double)]),
         'magot_plan_device_outputs': (ctypes.c_int, [_vp, ctypes.POINTER(_vp),
                                                      ctypes.POINTER(_vp)]),
         'magot_plan_algorithmic_bytes': (ctypes.c_uint64, [_vp]),
@@ -118,6 +120,8 @@ def _declare(lib):
         'magot_orf6_fetch': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
         'magot_orf6_time': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_double)]),
+        'magot_orf6_time_b2b': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_double)]),
         'magot_orf6_destroy': (None, [_vp]),
         'magot_fasta_text_create': (ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(_vp), _u64p]),
         'magot_fasta_text_execute': (ctypes.c_int, [_vp, _vp]),

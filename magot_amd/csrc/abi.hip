@@ -756,6 +756,26 @@ int magot_plan_time(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms) {
   return MAGOT_OK;
 }
 
+int magot_plan_time_b2b(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms) {
+  if (int rc = bind(ctx)) return rc;
+  if (!p || iters <= 0 || !avg_ms) {
+    set_error("magot_plan_time_b2b: bad argument");
+    return MAGOT_ERR_ARG;
+  }
+  // one event pair around `iters` back-to-back launches: the per-launch time
+  // of a step loop (no host round trip between launches)
+  MAGOT_HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+  for (int i = 0; i < iters; ++i) launch_extract(p->args, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  MAGOT_HIP_TRY(hipEventSynchronize(ctx->ev1));
+  float ms = 0.f;
+  MAGOT_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  p->executed = true;
+  *avg_ms = (double)ms / iters;
+  return MAGOT_OK;
+}
+
 int magot_plan_copy_outputs(magot_ctx* ctx, magot_plan* p, void* nuc_dst_dev, void* pep_dst_dev) {
   if (int rc = bind(ctx)) return rc;
   if (!p) {
@@ -1170,6 +1190,23 @@ int magot_orf6_time(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms) {
     total += ms;
   }
   *avg_ms = total / iters;
+  return MAGOT_OK;
+}
+
+int magot_orf6_time_b2b(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o || !avg_ms || iters <= 0) {
+    set_error("magot_orf6_time_b2b: bad argument");
+    return MAGOT_ERR_ARG;
+  }
+  MAGOT_HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+  for (int i = 0; i < iters; ++i) o->launch(ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  MAGOT_HIP_TRY(hipEventSynchronize(ctx->ev1));
+  float ms = 0;
+  MAGOT_HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  *avg_ms = (double)ms / iters;
   return MAGOT_OK;
 }
 

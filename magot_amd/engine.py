@@ -378,10 +378,30 @@ class ExtractionPlan(object):
             ctypes.c_void_p(nuc_dev_ptr) if nuc_dev_ptr else None,
             ctypes.c_void_p(pep_dev_ptr) if pep_dev_ptr else None), 'magot_plan_copy_outputs')
 
+    def fetch_to(self, nuc_addr=None, pep_addr=None):
+        """D2H of the outputs straight into caller host memory given by address
+        (e.g. pinned buffers); returns (nuc_off, pep_off)."""
+        noff = np.empty(self.n_tx + 1, dtype=np.uint64)
+        poff = np.empty(self.n_tx + 1, dtype=np.uint64)
+        check(_lib.lib().magot_plan_fetch(self.ctx.handle, self.handle,
+                                          ctypes.c_void_p(nuc_addr) if nuc_addr else None,
+                                          ptr(noff),
+                                          ctypes.c_void_p(pep_addr) if pep_addr else None,
+                                          ptr(poff)), 'magot_plan_fetch')
+        return noff, poff
+
     def time(self, iters):
+        """Mean duration of `iters` isolated launches (an event pair each)."""
         ms = ctypes.c_double()
         check(_lib.lib().magot_plan_time(self.ctx.handle, self.handle, int(iters),
                                          ctypes.byref(ms)), 'magot_plan_time')
+        return ms.value
+
+    def time_b2b(self, iters):
+        """Per-launch time of `iters` back-to-back launches (one event pair)."""
+        ms = ctypes.c_double()
+        check(_lib.lib().magot_plan_time_b2b(self.ctx.handle, self.handle, int(iters),
+                                             ctypes.byref(ms)), 'magot_plan_time_b2b')
         return ms.value
 
     @property
@@ -601,10 +621,26 @@ class Orf6Plan(object):
                                           ptr(slen)), 'magot_orf6_fetch')
         return out[:self.total], soff, slen[:6 * self.plan.n_tx]
 
+    def fetch_to(self, out_addr):
+        """D2H of the padded residue bytes into caller host memory (an address,
+        e.g. a pinned buffer of ``total`` bytes); returns (stream_off, stream_len)."""
+        soff = np.empty(6 * self.plan.n_tx + 1, dtype=np.uint64)
+        slen = np.empty(max(6 * self.plan.n_tx, 1), dtype=np.uint64)
+        check(_lib.lib().magot_orf6_fetch(self.ctx.handle, self.handle,
+                                          ctypes.c_void_p(out_addr) if out_addr else None,
+                                          ptr(soff), ptr(slen)), 'magot_orf6_fetch')
+        return soff, slen[:6 * self.plan.n_tx]
+
     def time(self, iters):
         ms = ctypes.c_double()
         check(_lib.lib().magot_orf6_time(self.ctx.handle, self.handle, int(iters),
                                          ctypes.byref(ms)), 'magot_orf6_time')
+        return ms.value
+
+    def time_b2b(self, iters):
+        ms = ctypes.c_double()
+        check(_lib.lib().magot_orf6_time_b2b(self.ctx.handle, self.handle, int(iters),
+                                             ctypes.byref(ms)), 'magot_orf6_time_b2b')
         return ms.value
 
     def close(self):

@@ -14,6 +14,10 @@
  *                               other strands / missing contig => None
  *   Sequence.reverse_compliment genome.py:784-793
  *   Sequence.translate          genome.py:795-822  frame 0, trimX
+ * and, per record sequence (oracle_orf6_compare):
+ *   Sequence.get_orfs           genome.py:824-851  translate(frame, strand)
+ *                               for frame 0,1,2 x strand '-','+' (any frame,
+ *                               either strand, trimX, None when len <= 2+frame)
  *
  * Build: gcc -O2 -shared -fPIC -o oracle/build/libcds_oracle.so oracle/cds_oracle.c
  */
@@ -147,4 +151,85 @@ int64_t oracle_extract(const unsigned char *genome, const int64_t *coff, int64_t
   free(keys);
   free(tmp);
   return w;
+}
+
+/*
+ * Sequence.translate (genome.py:795-822), literally: strand '-' reverse-
+ * complements first (:805-808); None (returns -1) unless len > 2 + frame
+ * (:809); for p in range(frame, len) the upper()ed residue joins the triplet
+ * and a codon is emitted when (p + frame) % 3 == 2 (:810-812), looked up in
+ * the standard code, 'X' for anything else -- a junk 1- or 2-char triplet, or
+ * one with a non-ACGT base (:813-816); trimX drops one leading 'X' (:819-821).
+ * tmp holds len bytes (the reverse complement).  Returns residues written.
+ */
+static int64_t translate_ref(const unsigned char *seq, int64_t len, int frame, int minus,
+                             unsigned char *tmp, unsigned char *out) {
+  if (!(len > 2 + frame)) return -1;
+  const unsigned char *s = seq;
+  if (minus) {
+    for (int64_t j = 0; j < len; ++j) tmp[j] = rc_map[seq[len - 1 - j]];
+    s = tmp;
+  }
+  int64_t w = 0;
+  int n = 0;
+  int code[3];
+  for (int64_t p = frame; p < len; ++p) {
+    if (n < 3) code[n] = code_map[s[p]];
+    ++n;
+    if ((p + frame) % 3 == 2) {
+      out[w++] = (n == 3 && code[0] >= 0 && code[1] >= 0 && code[2] >= 0)
+                     ? (unsigned char)aa_tab[16 * code[0] + 4 * code[1] + code[2]] : 'X';
+      n = 0;
+    }
+  }
+  if (w > 0 && out[0] == 'X') {
+    memmove(out, out + 1, (size_t)(w - 1));
+    --w;
+  }
+  return w;
+}
+
+/*
+ * Check six-frame device output against translate_ref for records
+ * [r0, r1) of n: record r is seq[seq_off[r] .. seq_off[r+1]).  Device stream
+ * j = 6r + 2f + (strand == '+') holds the residues at dev[stream_off[j] ..
+ * + stream_len[j]) in the layout of include/magot.h (magot_orf6_*): frames 1/2
+ * without their junk first codon, frame 0 untrimmed (one leading 'X' is
+ * dropped here before comparing), length 0 where the reference returns None.
+ * Returns the number of mismatching streams; *first_bad = the first one (or -1).
+ */
+int64_t oracle_orf6_compare(const unsigned char *seq, const int64_t *seq_off, int64_t r0,
+                            int64_t r1, const unsigned char *dev, const uint64_t *stream_off,
+                            const uint64_t *stream_len, int64_t *first_bad) {
+  init_tables();
+  int64_t bad = 0;
+  *first_bad = -1;
+  int64_t cap = 0;
+  unsigned char *tmp = NULL, *ref = NULL;
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t len = seq_off[r + 1] - seq_off[r];
+    if (len + 16 > cap) {
+      cap = 2 * len + 64;
+      tmp = (unsigned char *)realloc(tmp, (size_t)cap);
+      ref = (unsigned char *)realloc(ref, (size_t)cap);
+    }
+    for (int f = 0; f < 3; ++f) {
+      for (int plus = 0; plus < 2; ++plus) {
+        const int64_t j = 6 * r + 2 * f + plus;
+        const int64_t n = translate_ref(seq + seq_off[r], len, f, !plus, tmp, ref);
+        const unsigned char *g = dev + stream_off[j];
+        int64_t gl = (int64_t)stream_len[j];
+        if (f == 0 && gl > 0 && g[0] == 'X') { ++g; --gl; }
+        const int ok = n < 0 ? stream_len[j] == 0
+                             : (gl == n && (n == 0 || memcmp(g, ref, (size_t)n) == 0));
+        if (!ok) {
+          if (*first_bad < 0) *first_bad = j;
+          ++bad;
+        }
+      }
+    }
+  }
+  free(tmp);
+  free(ref);
+  return bad;
 }

@@ -37,6 +37,9 @@ def lib():
         L.oracle_extract.restype = ctypes.c_int64
         L.oracle_extract.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp,
                                      ctypes.c_int, vp, vp, vp]
+        L.oracle_orf6_compare.restype = ctypes.c_int64
+        L.oracle_orf6_compare.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp,
+                                          ctypes.POINTER(ctypes.c_int64)]
         _lib = L
     return _lib
 
@@ -83,3 +86,31 @@ def extract_workload(w, protein, tx_subset=None):
     c1 = w.ex_start[idx] + w.ex_len[idx]
     strand = np.where(w.tx_strand[tx_of] < 0, ord('-'), ord('+')).astype(np.uint8)
     return extract(w.genome, w.contig_off, rec_off, w.tx_contig[tx_of], c0, c1, strand, protein)
+
+
+def orf6_compare(seq, seq_off, dev_out, stream_off, stream_len, threads=1):
+    """Six-frame device output (magot_orf6_* layout) against the reference's
+    translate(frame, strand) for every record and frame (genome.py:795-851),
+    records split over ``threads`` threads (ctypes releases the GIL).
+    Returns (mismatching streams, first mismatching stream or -1)."""
+    from concurrent.futures import ThreadPoolExecutor
+    seq = np.ascontiguousarray(seq, dtype=np.uint8)
+    so = np.ascontiguousarray(seq_off, dtype=np.int64)
+    dev_out = np.ascontiguousarray(dev_out, dtype=np.uint8)
+    soff = np.ascontiguousarray(stream_off, dtype=np.uint64)
+    slen = np.ascontiguousarray(stream_len, dtype=np.uint64)
+    n = len(so) - 1
+    L = lib()
+    bounds = np.linspace(0, n, max(1, threads) + 1).astype(np.int64)
+
+    def run(i):
+        fb = ctypes.c_int64()
+        k = L.oracle_orf6_compare(_p(seq), _p(so), int(bounds[i]), int(bounds[i + 1]),
+                                  _p(dev_out), _p(soff), _p(slen), ctypes.byref(fb))
+        return k, fb.value
+
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        res = list(ex.map(run, range(len(bounds) - 1)))
+    bad = sum(k for k, _ in res)
+    firsts = [f for _, f in res if f >= 0]
+    return bad, (min(firsts) if firsts else -1)

@@ -9,6 +9,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
+# stages: tests slow bench driver c2 c5 multi kt kt5 kt2 pmc
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
 has() { [[ " $STAGES " == *" $1 "* ]]; }
@@ -23,6 +24,24 @@ fi
 if has bench; then
   timeout -k 10 900 python $BENCH > $OUT/bench.json 2> $OUT/bench.err || { tail -30 $OUT/bench.err; exit 1; }
   cat $OUT/bench.json
+fi
+if has driver; then
+  timeout -k 10 300 python $BENCH --steps 20 --warmup 5 > $OUT/bench_driver_cfg_20_5.json 2> $OUT/driver.err || { tail -30 $OUT/driver.err; exit 1; }
+  cat $OUT/bench_driver_cfg_20_5.json
+fi
+if has c2; then
+  timeout -k 10 300 python $BENCH --config C2 > $OUT/bench_c2.json 2> $OUT/c2.err || { tail -30 $OUT/c2.err; exit 1; }
+  cat $OUT/bench_c2.json
+fi
+if has c5; then
+  timeout -k 10 600 python $BENCH --config C5 > $OUT/bench_c5.json 2> $OUT/c5.err || { tail -30 $OUT/c5.err; exit 1; }
+  cat $OUT/bench_c5.json
+fi
+if has multi; then
+  # two ranks launched by bench itself, sharing the one card over gloo (the
+  # C4 orchestration; the driver's 8-GPU node runs it over RCCL)
+  MAGOT_DIST_BACKEND=gloo timeout -k 10 600 python $BENCH --gpus 2 --steps 50 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo2.json 2> $OUT/gloo2.err || { tail -30 $OUT/gloo2.err; exit 1; }
+  grep '^{' $OUT/bench_gloo2.json
 fi
 if has kt; then
   rm -rf $OUT/kt

@@ -1,0 +1,57 @@
+"""bench.py end to end on the GPU at test size: the one-rank job and the
+multi-rank C4 path that ``python bench.py --gpus N`` launches itself (two
+ranks rehearsed on one card with MAGOT_DIST_BACKEND=gloo; the RCCL path is the
+same code with the nccl backend, one GPU per rank).  Each rank checks its own
+shard against the C oracle, and rank 0 checks the outputs gathered from every
+rank in global record order."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _bench(args, env_extra=None):
+    env = dict(os.environ)
+    env.pop('WORLD_SIZE', None)
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{')]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+COMMON = ['--steps', '5', '--warmup', '1', '--settle-ms', '5', '--no-cpu-baseline']
+
+
+def test_bench_one_rank():
+    d = _bench(['--config', 'small'] + COMMON)
+    assert d['n_gpus'] == 1 and d['scaling'] == 'strong'
+    assert d['parity'].startswith('bit-exact'), d['parity']
+    assert d['value'] > 0 and d['roofline']['kernel_ms'] > 0
+    assert d['phases_s']['outputs_d2h_pinned'] > 0
+
+
+def test_bench_spawns_two_ranks_strong():
+    d = _bench(['--gpus', '2', '--config', 'small'] + COMMON,
+               {'MAGOT_DIST_BACKEND': 'gloo'})
+    assert d['n_gpus'] == 2 and d['scaling'] == 'strong'
+    assert d['parity'].startswith('bit-exact'), d['parity']
+    assert d['outputs_gather']['parity'].startswith('bit-exact'), d['outputs_gather']
+    assert d['load_imbalance'] < 0.05
+    assert d['genome_broadcast_s'] is not None
+    assert d['config']['parallelism'].startswith('contig-sharded x2')
+
+
+def test_bench_spawns_two_ranks_weak():
+    d = _bench(['--gpus', '2', '--config', 'small', '--mode', 'weak'] + COMMON,
+               {'MAGOT_DIST_BACKEND': 'gloo'})
+    assert d['n_gpus'] == 2 and d['scaling'] == 'weak'
+    assert d['parity'].startswith('bit-exact'), d['parity']

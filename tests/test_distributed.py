@@ -1,10 +1,12 @@
 """The bench's multi-rank path on CPU: world_size 2 over gloo (127.0.0.1).
 
-bench.py --gpus N runs one process per GPU; each rank extracts its own
-contig shard (weak scaling) and torch.distributed is used only for the
-barrier and the max/sum reductions.  These tests run that orchestration with
-the gloo backend: rendezvous, the reductions bench.py reports from, and that
-rank shards are distinct, deterministic workloads.
+bench.py --gpus N runs one process per GPU (started by bench itself, or by
+torchrun); by default the N ranks share ONE job (C4: genome broadcast,
+records sharded in genome order, outputs returned per rank or gathered to
+rank 0).  These tests run that orchestration with the gloo backend:
+rank launching and failure propagation, rendezvous, the reductions bench.py
+reports from, the record sharding on C3's own tables, the byte gather and
+the reassembly into global record order.
 """
 import os
 import socket
@@ -31,7 +33,7 @@ def _worker(rank, world, port, out):
                        'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
     import bench
     from magot_amd import synth
-    dist, r, local, n = bench.dist_setup(world)
+    dist, r, local, n = bench.dist_setup()
     assert (r, local, n) == (rank, rank, world)
     assert dist.get_backend() == 'gloo'
     bench.barrier(dist)
@@ -96,12 +98,68 @@ def test_record_shards_partition_records():
     rng = np.random.default_rng(6)
     tx_contig = rng.integers(0, 20, size=5000)
     tx_bases = rng.integers(50, 3000, size=5000)
-    owner, shards, load = shard.record_shards(tx_contig, tx_bases, 20, 4)
+    tx_start = rng.integers(0, 10**6, size=5000)
+    shards, load, spans = shard.record_shards(tx_contig, tx_bases, 20, 4, tx_start=tx_start)
     allrec = np.sort(np.concatenate(shards))
     assert np.array_equal(allrec, np.arange(5000))
     for r, sh in enumerate(shards):
-        assert np.all(owner[tx_contig[sh]] == r)           # whole contigs per rank
         assert np.all(np.diff(sh) > 0)                      # global order kept
+        assert load[r] == tx_bases[sh].sum()
+        # one genome range per rank: (contig, start) of its records is contiguous
+        key = tx_contig * 10**7 + tx_start
+        lo, hi = key[sh].min(), key[sh].max()
+        others = np.setdiff1d(np.arange(5000), sh)
+        assert not np.any((key[others] > lo) & (key[others] < hi))
+    assert shard.imbalance(load) < 0.01
+    for c in range(20):
+        ranks = [r for r in range(4) if np.any(tx_contig[shards[r]] == c)]
+        assert (spans[c, 0], spans[c, 1]) == (min(ranks), max(ranks))
+
+
+def test_record_shards_c3_balance():
+    """C3's own tables (seed 20261018): its largest contig holds 23 % of the
+    CDS bases, so contig-granular LPT was 86 % imbalanced at 8 ranks; the
+    genome-order ranges split it and stay far below 5 % at 2, 4 and 8."""
+    from magot_amd import shard, synth
+    w = synth.make('C3')
+    assert synth.SEED_BASE + 3 == 20261018
+    first = np.zeros(w.n_tx + 1, dtype=np.int64)
+    np.cumsum(w.ex_count, out=first[1:])
+    tx_bases = np.add.reduceat(w.ex_len, first[:-1])
+    per_contig = np.bincount(w.tx_contig, weights=tx_bases)
+    assert per_contig.max() / per_contig.sum() > 0.2            # the oversized contig
+    for n in (2, 4, 8):
+        shards, load, spans = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), n,
+                                                  tx_start=w.ex_start[first[:-1]])
+        assert shard.imbalance(load) < 0.05, (n, shard.imbalance(load))
+        assert sum(len(s) for s in shards) == w.n_tx
+        assert load.sum() == w.cds_bases
+        assert np.any(spans[:, 0] != spans[:, 1])               # a contig spans ranks
+        del shards
+
+
+def test_reassemble_split_contig_global_order():
+    """Per-rank outputs of a sharded job (oracle extraction of each shard)
+    put back together equal the single-job output, with contigs split."""
+    from magot_amd import shard, synth
+    from oracle import cds_oracle
+    w = synth.make('small', seed=11, genome_bases=300_000, n_tx=400)
+    first = np.zeros(w.n_tx + 1, dtype=np.int64)
+    np.cumsum(w.ex_count, out=first[1:])
+    tx_bases = np.add.reduceat(w.ex_len, first[:-1])
+    shards, load, spans = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), 5,
+                                              tx_start=w.ex_start[first[:-1]])
+    assert np.any(spans[:, 0] != spans[:, 1])
+    for protein in (False, True):
+        full, foff, _ = cds_oracle.extract_workload(w, protein)
+        parts, offs = [], []
+        for sh in shards:
+            out, off, st = cds_oracle.extract_workload(w, protein, tx_subset=sh)
+            assert not st.any()
+            parts.append(out)
+            offs.append(off)
+        got, goff = shard.reassemble(shards, parts, offs)
+        assert np.array_equal(got, full) and np.array_equal(goff, foff)
 
 
 def test_reassemble_round_trip():
@@ -153,3 +211,65 @@ def test_gather_bytes_two_ranks_gloo():
     for r in range(world):
         n = 10 + 7 * r
         assert got[r] == [(i + r) & 0xFF for i in range(n)]
+
+
+# ---------------------------------------------------------------------------
+# bench.py launching its own ranks (python bench.py --gpus N, no torchrun)
+# ---------------------------------------------------------------------------
+
+_CHILD = r"""
+import json, os, sys
+sys.path.insert(0, %(root)r)
+import bench
+dist, rank, local, world = bench.dist_setup()
+assert (rank, local) == (int(os.environ['RANK']), int(os.environ['LOCAL_RANK']))
+assert dist.get_backend() == 'gloo'
+fail = int(sys.argv[1]) if len(sys.argv) > 1 else -1
+if rank == fail:
+    sys.exit(3)
+bench.barrier(dist)
+s = bench.allreduce_sum(dist, float(rank + 1))
+if rank == 0:
+    print(json.dumps({'n_gpus': world, 'sum': s}), flush=True)
+dist.destroy_process_group()
+"""
+
+
+def _launch(tmp_path, n, argv):
+    import subprocess
+    child = tmp_path / 'child.py'
+    child.write_text(_CHILD % {'root': ROOT})
+    code = ('import sys; sys.path.insert(0, %r); import bench; '
+            'sys.exit(bench.spawn_ranks(%d, %r, script=%r))' % (ROOT, n, argv, str(child)))
+    env = dict(os.environ, MAGOT_DIST_BACKEND='gloo')
+    env.pop('WORLD_SIZE', None)
+    return subprocess.run([sys.executable, '-c', code], env=env, capture_output=True,
+                          text=True, timeout=180)
+
+
+def test_spawn_ranks_two_gloo(tmp_path):
+    import json
+    r = _launch(tmp_path, 2, [])
+    assert r.returncode == 0, r.stderr
+    # gloo itself prints "[Gloo] Rank 0 is connected ..." on stdout
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{')]
+    assert len(lines) == 1                                   # rank 0's line only
+    assert json.loads(lines[0]) == {'n_gpus': 2, 'sum': 3.0}
+
+
+def test_spawn_ranks_failure_propagates(tmp_path):
+    # rank 1 exits 3 while rank 0 waits in a barrier: the launcher reports
+    # 3 and terminates rank 0 instead of hanging
+    r = _launch(tmp_path, 2, ['1'])
+    assert r.returncode == 3
+    assert '{' not in r.stdout
+
+
+def test_bench_refuses_more_ranks_than_devices(tmp_path):
+    import subprocess
+    env = dict(os.environ)
+    env.pop('WORLD_SIZE', None)
+    env.pop('MAGOT_DIST_BACKEND', None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2'],
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 2 and 'device(s) visible' in r.stderr

@@ -300,9 +300,11 @@ def test_tiny_exons_and_lds_overflow_vs_c_oracle():
     check_against_oracle(w)
 
 
-def test_c2_shape_nucleotide_only():
+def test_c2_full_size_nucleotide_only():
+    """BASELINE configs[1] at its stated size: 100 Mb, 50k single-exon CDS."""
     from oracle import cds_oracle
-    w = synth.make('C2', genome_bases=20_000_000, n_tx=10_000)
+    w = synth.make('C2')
+    assert w.n_tx == 50_000 and int(w.contig_len.sum()) == 100_000_000
     nuc, noff, pep, poff = gpu_extract(w, engine.OUT_NUC)
     ref, roff, st = cds_oracle.extract_workload(w, False)
     assert pep is None
@@ -314,6 +316,28 @@ def test_c3_full_size_vs_c_oracle():
     """The headline workload (1 Gb genome, 500k transcripts), byte for byte."""
     w = synth.make('C3')
     check_against_oracle(w)
+
+
+@pytest.mark.slow
+def test_c5_full_size_six_frames_vs_c_oracle():
+    """BASELINE configs[4] at its stated size (3 Gb genome, 2M transcripts):
+    the fused gather + six-frame kernel, ALL six frames of ALL records against
+    the C oracle's translate(frame, strand) (genome.py:795-851)."""
+    from oracle import cds_oracle
+    w = synth.make('C5')
+    dev = engine.DeviceGenome(w.contigs())
+    ex, tx = w.plan_tables()
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    o6.close()
+    plan.close()
+    dev.close()
+    ref, roff, st = cds_oracle.extract_workload(w, False)
+    assert not st.any()
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or min(16, os.cpu_count() or 1)
+    assert cds_oracle.orf6_compare(ref, roff, out, soff, slen, threads=threads) == (0, -1)
 
 
 @pytest.mark.parametrize('paths', ['1', '2', '3'])

@@ -8,6 +8,7 @@ import hashlib
 import json
 import os
 
+import numpy as np
 import pytest
 
 import goldlib
@@ -180,3 +181,32 @@ def test_c_oracle_matches_python_oracle():
         seqs = text.split('\n')[1::2]
         got = [out[off[i]:off[i + 1]].tobytes().decode('latin-1') for i in range(w.n_tx)]
         assert got == seqs
+
+
+def test_c_oracle_six_frames_vs_reference_kats():
+    """oracle_orf6_compare's translate(frame, strand) (cds_oracle.c) against
+    the reference's own outputs in kat.json (frames 0-2, both strands, with
+    and without trimX), laid out as the device streams are: frame 0
+    untrimmed, frames 1/2 without their junk codon (= trimmed)."""
+    from oracle import cds_oracle
+    kats = _json('kat.json')
+    seqs = [k['seq'] for k in kats]
+    buf = np.frombuffer(''.join(seqs).encode('latin-1'), dtype=np.uint8)
+    off = np.zeros(len(seqs) + 1, dtype=np.int64)
+    np.cumsum([len(x) for x in seqs], out=off[1:])
+    streams = []
+    for k in kats:
+        for f in (0, 1, 2):
+            for st in ('-', '+'):
+                v = k['translate']['%d%s%d' % (f, st, 0 if f == 0 else 1)]
+                streams.append(v or '')
+    slen = np.array([len(x) for x in streams], dtype=np.uint64)
+    soff = np.zeros(len(streams) + 1, dtype=np.uint64)
+    np.cumsum(slen, out=soff[1:])
+    dev = np.frombuffer(''.join(streams).encode('latin-1') + b'\0', dtype=np.uint8)
+    assert cds_oracle.orf6_compare(buf, off, dev, soff, slen, threads=2) == (0, -1)
+    # a flipped residue is caught, in the right stream
+    j = next(i for i, x in enumerate(streams) if x)
+    bad = dev.copy()
+    bad[int(soff[j]) + len(streams[j]) - 1] ^= 0x20
+    assert cds_oracle.orf6_compare(buf, off, bad, soff, slen)[1] == j
