@@ -383,6 +383,18 @@ def run_job(args, dist, rank, local, world):
 
     mine, imb, t_bcast, t_pack = None, 0.0, None, None
     shards = None
+    rehearse = None
+    if args.rehearse_shard and world == 1:
+        # diagnostic: this single GPU runs rank r's shard of a K-rank C4 job
+        # (what each GPU of the 8-GPU node gets), genome packed locally
+        k, r = (int(x) for x in args.rehearse_shard.split(':'))
+        first = np.zeros(w.n_tx + 1, dtype=np.int64)
+        np.cumsum(w.ex_count, out=first[1:])
+        tx_bases = np.add.reduceat(w.ex_len, first[:-1])
+        sh, load, _ = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), k,
+                                          tx_start=w.ex_start[first[:-1]])
+        mine = sh[r]
+        rehearse = {'ranks': k, 'rank': r, 'load_imbalance': shard.imbalance(load)}
     if strong and world > 1:
         first = np.zeros(w.n_tx + 1, dtype=np.int64)
         np.cumsum(w.ex_count, out=first[1:])
@@ -549,6 +561,10 @@ def run_job(args, dist, rank, local, world):
             'outputs_d2h_bases_per_s': total_bases / t_d2h if t_d2h else None,
             'output_bytes_rank0': out_bytes,
         }
+        if rehearse:
+            rec['rehearsal'] = rehearse
+            rec['config']['workload'] = 'REHEARSAL (not a bench line): rank %d of a %d-rank ' \
+                '%s job on one GPU' % (rehearse['rank'], rehearse['ranks'], args.config)
         if strong and world > 1:
             rec['genome_broadcast_s'] = t_bcast
             rec['load_imbalance'] = imb
@@ -629,8 +645,13 @@ def main(argv=None):
     ap.add_argument('--mode', default='strong', choices=['strong', 'weak'],
                     help='strong (default): one job over N GPUs, genome broadcast, records '
                          'sharded (C3 at N=1, C4 at N>1); weak: one job per rank')
+    ap.add_argument('--rehearse-shard', default=None, metavar='K:r',
+                    help='diagnostic, one GPU: run only rank r\'s shard of a K-rank strong job '
+                         '(the per-GPU work of the K-GPU line; not a bench line)')
     raw = sys.argv[1:] if argv is None else argv
     args = ap.parse_args(raw)
+    if args.rehearse_shard and args.gpus > 1:
+        ap.error('--rehearse-shard runs one rank')
     if args.pmc_json is None:
         args.pmc_json = os.path.join(ROOT, 'profiles', 'pmc_%s.json' % args.config)
 

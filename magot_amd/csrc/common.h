@@ -95,6 +95,7 @@ constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the til
 #define MAGOT_EXP_EXON_CAP 128
 #endif
 constexpr int kExonCap = MAGOT_EXP_EXON_CAP;  // intervals staged in LDS per tile (7 blocks of 4 waves fit a CU's LDS)
+static_assert((kExonCap & (kExonCap - 1)) == 0, "kExonCap must be a power of two (row index masks)");
 constexpr int kTxCap = 64;                    // records staged in LDS per tile
 constexpr int kPepSlots = 64 * kPepPerLane;  // residue chunks per tile
 constexpr uint64_t kExcBit = 1ull << 62;      // interval touches an exception run
@@ -164,6 +165,10 @@ struct ExtractArgs {
 
 // Wave-wide inclusive prefix sum with DPP row shifts and row broadcasts
 // (gfx9 wave64: row_shr:1/2/4/8 inside rows of 16, then row_bcast:15/31).
+// The row_bcast controls exist only on gfx9 (CDNA) wave64 targets.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "wave_scan uses DPP row_bcast:15/31, which exists only on gfx9 wave64 (gfx950) targets"
+#endif
 __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);

@@ -543,18 +543,11 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     // every candidate offset computed unconditionally (selects, no branches
     // around LDS reads)
     uint32_t fa = X.x + c8, ra = L.vb[i] - c8;
-    const uint32_t ib = (uint32_t)min(i + 1, (int)d.m - 1) & (kExonCap - 1);  // < kExonCap
+    const uint32_t ib = (uint32_t)min(i + 1, (int)d.m - 1) & (kExonCap - 1);  // < kExonCap (a power of two)
     uint32_t fb2 = Y.x + c8, rb = L.vb[ib] - c8;
     __asm__("" : "+v"(fa), "+v"(ra), "+v"(fb2), "+v"(rb));
-#ifdef MAGOT_EXP_HALF
-    // diagnostic (wrong output): windows at half the plane density, the
-    // footprint of a 2-bit plane
-    const uint32_t offa = ((rev ? ra : fa) >> 1) & ~3u;
-    const uint32_t offb = two ? (((rev ? rb : fb2) >> 1) & ~3u) : offa;
-#else
     const uint32_t offa = rev ? ra : fa;
     const uint32_t offb = two ? (rev ? rb : fb2) : offa;
-#endif
     const uint32_t sha = (rev ? X.w >> 5 : X.w) & 0x700u, shb = (rev ? fb >> 5 : fb) & 0x700u;
     // mask index: segment A's bytes are the low n1 nibbles, or (reversed) the
     // high n1 nibbles (s_mask[17 + n1])

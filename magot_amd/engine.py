@@ -120,8 +120,11 @@ class DeviceGenome(object):
 
 
 # One device plane addresses < 4 Gbases (32-bit window offsets, extract.hip);
-# a larger genome is packed as several planes (PartitionedGenome).
-PART_BASES = int(os.environ.get('MAGOT_GENOME_PART_BASES', '3500000000'))
+# a larger genome is packed as several planes (PartitionedGenome).  The C side
+# refuses a plane whose packed span (kOrigin=64 pad bases + bases + 256) reaches
+# 0xFFFFFFF0 (magot_genome_load), so the part size is clamped below that.
+PLANE_LIMIT = 0xFFFFFFF0 - 64 - 256 - 1
+PART_BASES = min(int(os.environ.get('MAGOT_GENOME_PART_BASES', '3500000000')), PLANE_LIMIT)
 
 
 def plan_parts(lengths, limit=None):

@@ -72,11 +72,14 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
     lg, gm = _literal(longest), _literal(genomic)
     if (native == 'True' and isinstance(lg, bool) and isinstance(gm, bool) and
             seq_type in ('nucleotide', 'protein')):
-        text = _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=lg is True,
-                                 genomic=gm is True, from_exons=from_exons == 'True')
+        text, parsed = _gff2fasta_native(genome_sequence, gff, seq_type, order,
+                                         longest=lg is True, genomic=gm is True,
+                                         from_exons=from_exons == 'True')
         if text is not None:
             _write_bytes(text, b'\n')
             return
+        if parsed is not None:
+            genome_sequence = parsed  # read once: the object path reuses it
     g = genome.Genome(genome_sequence)
     if from_exons == 'True':
         # reference quirk kept: a str features_to_ignore is a substring test
@@ -90,24 +93,29 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
 
 def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, genomic=False,
                       from_exons=False):
-    """The gff2fasta text (bytes) via the native planner, the extraction
-    kernel and device text assembly, or None when the planner declines."""
+    """(text, parsed): the gff2fasta text (bytes) via the native planner, the
+    extraction kernel and device text assembly, or (None, GenomeSequence or
+    None) when it declines -- the GenomeSequence already parsed, for the
+    object path to reuse."""
     if order not in ('py2', 'insertion'):
         raise ValueError("order must be 'insertion' or 'py2'")
     # the FASTA is read and packed natively; Python reader for unusual headers
     dev = engine.FastaGenome.load(genome.read_buffer(genome_sequence))
+    seqs = None
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)
+        if sum(len(v) for v in seqs.values()) > engine.PART_BASES:
+            # several device planes: the object path extracts per plane;
+            # decided before anything is packed
+            return None, seqs
         dev = seqs.device()
-        if isinstance(dev, engine.PartitionedGenome):
-            return None  # several device planes: the object path extracts per plane
     names = dev.names
     protein = seq_type == 'protein'
     plan = engine.GffPlan.build(genome.read_buffer(gff), names, [int(x) for x in dev.lengths],
                                 protein=protein, order=order, longest=longest, genomic=genomic,
                                 from_exons=from_exons)
     if plan is None:
-        return None
+        return None, seqs
     try:
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                    engine.OUT_PEP if plan.protein else engine.OUT_NUC)
@@ -115,14 +123,14 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
             # longest=True over peptides: the render picks from the trimmed
             # lengths, on the host
             try:
-                return plan.render(*ex.run())
+                return plan.render(*ex.run()), None
             finally:
                 ex.close()
         text = engine.FastaText(plan, ex)
         try:
             ex.execute()
             text.execute()  # records + headers + joiners in one device buffer
-            return text.fetch()
+            return text.fetch(), None
         finally:
             text.close()
             ex.close()

@@ -35,7 +35,7 @@ def main():
     if a.whole:
         from magot_amd import genome_tools
         t = time.perf_counter()
-        text = genome_tools._gff2fasta_native(fa, gf, a.seq_type, a.order)
+        text = genome_tools._gff2fasta_native(fa, gf, a.seq_type, a.order)[0]
         total = time.perf_counter() - t
         with open(os.path.join(a.dir, 'out.fa'), 'rb') as fh:
             same = fh.read() == bytes(text) + b'\n'

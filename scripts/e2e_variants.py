@@ -24,14 +24,14 @@ def main():
     ap.add_argument('--dir', default='/tmp/magot_e2e')
     a = ap.parse_args()
     fa, gf = os.path.join(a.dir, 'genome.fa'), os.path.join(a.dir, 'ann.gff3')
-    genome_tools._gff2fasta_native(fa, gf, 'nucleotide', 'py2')  # warm: device start-up
+    genome_tools._gff2fasta_native(fa, gf, 'nucleotide', 'py2')[0]  # warm: device start-up
     rec = {}
     for name, st, kw in (('default_nucleotide', 'nucleotide', {}),
                          ('longest_nucleotide', 'nucleotide', {'longest': True}),
                          ('longest_protein', 'protein', {'longest': True}),
                          ('genomic', 'nucleotide', {'genomic': True})):
         t = time.perf_counter()
-        text = genome_tools._gff2fasta_native(fa, gf, st, 'py2', **kw)
+        text = genome_tools._gff2fasta_native(fa, gf, st, 'py2', **kw)[0]
         rec[name] = {'s': time.perf_counter() - t, 'native': text is not None,
                      'bytes': None if text is None else int(len(text)) + 1}
         if name == 'default_nucleotide':  # the CDS FASTA cds2pep reads below
