@@ -452,9 +452,12 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     uint32_t wa[kPer][3], wb[kPer][3], xa[kPer][2], xb[kPer][2];
     // Windows without a flagged interval (most) skip the exception plane:
     // no loads, no address math, no merge (wave-uniform).
+    // (the 64-bit ballot is tested before readfirstlane, which takes 32 bits:
+    // testing after it dropped rows 32-63 and 96-127, and a window whose only
+    // flagged interval sat there decoded its exceptions as 'A')
     const bool wexc = __builtin_amdgcn_readfirstlane(
                           __ballot((in[0] && (rw[0].y & kOrf6ExcRow)) ||
-                                   (in[1] && (rw[1].y & kOrf6ExcRow)))) != 0;
+                                   (in[1] && (rw[1].y & kOrf6ExcRow))) != 0);
     auto issue = [&](auto exc_tag) {
       constexpr bool kExc = decltype(exc_tag)::value;
 #pragma unroll

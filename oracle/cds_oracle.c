@@ -196,11 +196,13 @@ static int64_t translate_ref(const unsigned char *seq, int64_t len, int frame, i
  * + stream_len[j]) in the layout of include/magot.h (magot_orf6_*): frames 1/2
  * without their junk first codon, frame 0 untrimmed (one leading 'X' is
  * dropped here before comparing), length 0 where the reference returns None.
- * Returns the number of mismatching streams; *first_bad = the first one (or -1).
+ * Returns the number of mismatching streams; *first_bad = the first one (or -1),
+ * and the first bad_cap of them in bad_list (may be NULL).
  */
 int64_t oracle_orf6_compare(const unsigned char *seq, const int64_t *seq_off, int64_t r0,
                             int64_t r1, const unsigned char *dev, const uint64_t *stream_off,
-                            const uint64_t *stream_len, int64_t *first_bad) {
+                            const uint64_t *stream_len, int64_t *first_bad, int64_t *bad_list,
+                            int64_t bad_cap) {
   init_tables();
   int64_t bad = 0;
   *first_bad = -1;
@@ -224,6 +226,7 @@ int64_t oracle_orf6_compare(const unsigned char *seq, const int64_t *seq_off, in
                              : (gl == n && (n == 0 || memcmp(g, ref, (size_t)n) == 0));
         if (!ok) {
           if (*first_bad < 0) *first_bad = j;
+          if (bad_list && bad < bad_cap) bad_list[bad] = j;
           ++bad;
         }
       }

@@ -39,7 +39,7 @@ def lib():
                                      ctypes.c_int, vp, vp, vp]
         L.oracle_orf6_compare.restype = ctypes.c_int64
         L.oracle_orf6_compare.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp,
-                                          ctypes.POINTER(ctypes.c_int64)]
+                                          ctypes.POINTER(ctypes.c_int64), vp, ctypes.c_int64]
         _lib = L
     return _lib
 
@@ -88,11 +88,13 @@ def extract_workload(w, protein, tx_subset=None):
     return extract(w.genome, w.contig_off, rec_off, w.tx_contig[tx_of], c0, c1, strand, protein)
 
 
-def orf6_compare(seq, seq_off, dev_out, stream_off, stream_len, threads=1):
+def orf6_compare(seq, seq_off, dev_out, stream_off, stream_len, threads=1, bad_list=None):
     """Six-frame device output (magot_orf6_* layout) against the reference's
     translate(frame, strand) for every record and frame (genome.py:795-851),
     records split over ``threads`` threads (ctypes releases the GIL).
-    Returns (mismatching streams, first mismatching stream or -1)."""
+    Returns (mismatching streams, first mismatching stream or -1); with a list
+    as ``bad_list``, the mismatching stream ids (up to 1000 per thread) are
+    appended to it."""
     from concurrent.futures import ThreadPoolExecutor
     seq = np.ascontiguousarray(seq, dtype=np.uint8)
     so = np.ascontiguousarray(seq_off, dtype=np.int64)
@@ -105,8 +107,12 @@ def orf6_compare(seq, seq_off, dev_out, stream_off, stream_len, threads=1):
 
     def run(i):
         fb = ctypes.c_int64()
+        bl = np.full(1000, -1, dtype=np.int64)
         k = L.oracle_orf6_compare(_p(seq), _p(so), int(bounds[i]), int(bounds[i + 1]),
-                                  _p(dev_out), _p(soff), _p(slen), ctypes.byref(fb))
+                                  _p(dev_out), _p(soff), _p(slen), ctypes.byref(fb), _p(bl),
+                                  len(bl))
+        if bad_list is not None:
+            bad_list.extend(int(x) for x in bl[bl >= 0])
         return k, fb.value
 
     with ThreadPoolExecutor(max(1, threads)) as ex:

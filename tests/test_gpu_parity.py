@@ -466,6 +466,28 @@ def test_orf6_over_extraction_plan_vs_oracle():
     dev.close()
 
 
+def test_orf6_flag_in_upper_lanes_vs_oracle():
+    """Windows whose only exception-flagged interval is staged by lanes 32-63
+    (or 96-127): the wave-wide test of the flags once dropped those lanes and
+    decoded the N runs as 'A' (found by the full-size C5 check)."""
+    from oracle import cds_oracle
+    from test_orf6_plan import orf6_windows, upper_lane_workload, upper_only
+    w = upper_lane_workload()
+    assert upper_only(orf6_windows(w)) >= 20
+    dev = engine.DeviceGenome(w.contigs())
+    ex, tx = w.plan_tables()
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    ref, roff, st = cds_oracle.extract_workload(w, False)
+    assert not st.any()
+    assert cds_oracle.orf6_compare(ref, roff, out, soff, slen, threads=4) == (0, -1)
+    o6.close()
+    plan.close()
+    dev.close()
+
+
 def test_orf6_fused_gather_tiny_intervals_vs_oracle():
     """The fused gather over 1-6 base intervals on both strands (many
     intervals per 16-base vector, windows shortened to the interval cap) and
