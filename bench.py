@@ -423,7 +423,7 @@ def run_job(args, dist, rank, local, world):
     t_plan = time.perf_counter() - t0
     B, P = plan.nuc_bytes, plan.pep_bytes
     if c5:
-        _, _, slen = o6.fetch_to(None)
+        _, slen = o6.fetch_to(None)
         R = int(slen.sum())
         # algorithmic bytes: 2-bit genome reads + six translations + descriptors
         alg = -(-B // 4) + R + 16 * int(plan.n_exons) + 32 * int(plan.n_tx)

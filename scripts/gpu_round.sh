@@ -49,6 +49,13 @@ if has kt; then
   grep -h extract_kernel $OUT/kt/kt_kernel_stats.csv
   cat $OUT/kt.json
 fi
+for cfg in C5 C2; do
+  if has kt${cfg:1}; then
+    rm -rf $OUT/kt_$cfg
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$cfg -o kt -- python $BENCH --config $cfg --no-cpu-baseline > $OUT/kt_$cfg.json 2> $OUT/kt_$cfg.err || { tail -30 $OUT/kt_$cfg.err; exit 1; }
+    grep -h "orf6_kernel\|extract_kernel" $OUT/kt_$cfg/kt_kernel_stats.csv
+  fi
+done
 if has pmc; then
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" \
