@@ -421,7 +421,8 @@ def run_job(args, dist, rank, local, world):
     plan = engine.ExtractionPlan(dev, ex, tx, outputs)
     o6 = engine.Orf6Plan(plan) if c5 else None
     t_plan = time.perf_counter() - t0
-    B, P = plan.nuc_bytes, plan.pep_bytes
+    B = plan.nuc_bytes
+    P = plan.pep_bytes if outputs & engine.OUT_PEP else 0
     if c5:
         _, slen = o6.fetch_to(None)
         R = int(slen.sum())
