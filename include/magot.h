@@ -250,6 +250,20 @@ int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* s
                           const uint64_t* pep_off, uint8_t* out);
 
 /*
+ * Sequence.translate with an arbitrary codon `library` (genome.py:795-818:
+ * any dict -- keys that are not ACGT triplets, e.g. 'NNN', multi-character
+ * values -- and any integer frame, negative included).  The caller lays out
+ * the characters the reference's loop visits and drops the first (junk)
+ * codon; this computes one symbol per full codon of seq[0, 3*n_codons):
+ * out[k] = lut[c0 + K*c1 + K*K*c2], c = class256[byte] (upper-case folding
+ * and the library's key characters folded into K = n_classes classes,
+ * K^3 <= 32768).  The caller maps symbols to the library's values.
+ */
+int magot_codon_symbols(magot_ctx* ctx, const uint8_t* seq, uint64_t n_codons,
+                        const uint8_t* class256, uint32_t n_classes, const uint8_t* lut,
+                        uint8_t* out);
+
+/*
  * Six-frame translation for Sequence.get_orfs (genome.py:824-851): for each
  * record, translate(frame=f, strand) for f = 0,1,2 and strand '-','+' in the
  * reference's loop order.  Stream j = 6*record + 2*f + (strand == '+') holds

@@ -931,6 +931,45 @@ int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* s
   return rc;
 }
 
+int magot_codon_symbols(magot_ctx* ctx, const uint8_t* seq, uint64_t n_codons,
+                        const uint8_t* class256, uint32_t n_classes, const uint8_t* lut,
+                        uint8_t* out) {
+  if (int rc = bind(ctx)) return rc;
+  const uint64_t nl = (uint64_t)n_classes * n_classes * n_classes;
+  if (!class256 || !lut || n_classes == 0 || nl > kMaxSymbolLut || (n_codons && (!seq || !out))) {
+    set_error("magot_codon_symbols: bad argument");
+    return MAGOT_ERR_ARG;
+  }
+  for (int b = 0; b < 256; ++b)
+    if (class256[b] >= n_classes) {
+      set_error("magot_codon_symbols: class out of range");
+      return MAGOT_ERR_ARG;
+    }
+  if (n_codons == 0) return MAGOT_OK;
+  const uint64_t in_bytes = 3 * n_codons;
+  void* d = nullptr;
+  MAGOT_HIP_TRY(hipMalloc(&d, in_bytes + n_codons + 256 + nl + 64));
+  uint8_t* d_in = static_cast<uint8_t*>(d);
+  uint8_t* d_out = d_in + in_bytes;
+  uint8_t* d_cls = d_out + n_codons;
+  uint8_t* d_lut = d_cls + 256;
+  hipError_t e = hipMemcpyAsync(d_in, seq, in_bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_cls, class256, 256, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_lut, lut, nl, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) {
+    launch_codon_symbols(d_in, n_codons, d_cls, n_classes, d_lut, d_out, ctx->stream);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_out, n_codons, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  (void)hipFree(d);
+  if (e != hipSuccess) {
+    set_error(std::string("magot_codon_symbols: ") + hipGetErrorString(e));
+    return MAGOT_ERR_HIP;
+  }
+  return MAGOT_OK;
+}
+
 // --- six-frame translation (Sequence.get_orfs, genome.py:824-851) ----------
 
 int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,

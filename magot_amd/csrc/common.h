@@ -253,6 +253,11 @@ void launch_exc1(const uint32_t* nib, uint64_t nib_words, uint32_t* exc1, hipStr
 void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const int32_t* frames,
                       const uint8_t* strands, const uint64_t* pep_off, uint64_t total_pep,
                       const uint32_t* lut16, uint8_t* out, hipStream_t s);
+// Codon symbols over an extended alphabet (magot_codon_symbols): K classes,
+// K^3 <= kMaxSymbolLut.
+constexpr uint32_t kMaxSymbolLut = 32768;
+void launch_codon_symbols(const uint8_t* in, uint64_t n_codons, const uint8_t* cls, uint32_t K,
+                          const uint8_t* lut, uint8_t* out, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // FASTA text assembly (render.hip, gffplan.cpp)

@@ -829,6 +829,30 @@ void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t
                      total, out);
 }
 
+// Codon symbols over an extended alphabet (Sequence.translate with an
+// arbitrary `library`, genome.py:795-818): byte -> class through a 256-entry
+// table (upper-case folding and every character of the library's 3-char keys
+// included), codon index c0 + K*c1 + K*K*c2, symbol = lut[index].  One lane
+// per codon; the table and the LUT are staged in LDS by each block.
+__global__ __launch_bounds__(256) void codon_symbols_kernel(const uint8_t* __restrict__ in,
+                                                            uint64_t n_codons,
+                                                            const uint8_t* __restrict__ cls,
+                                                            uint32_t K,
+                                                            const uint8_t* __restrict__ lut,
+                                                            uint8_t* __restrict__ out) {
+  __shared__ uint8_t s_cls[256];
+  __shared__ uint8_t s_lut[kMaxSymbolLut];
+  s_cls[threadIdx.x] = cls[threadIdx.x];
+  const uint32_t nl = K * K * K;
+  for (uint32_t i = threadIdx.x; i < nl; i += 256) s_lut[i] = lut[i];
+  __syncthreads();
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= n_codons) return;
+  const uint8_t* p = in + 3 * k;
+  const uint32_t x = s_cls[p[0]] + K * (s_cls[p[1]] + K * s_cls[p[2]]);
+  out[k] = s_lut[x];
+}
+
 void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const int32_t* frames,
                       const uint8_t* strands, const uint64_t* pep_off, uint64_t total_pep,
                       const uint32_t* lut16, uint8_t* out, hipStream_t s) {
@@ -839,6 +863,14 @@ void launch_translate(const uint8_t* in, const uint64_t* off, uint64_t n, const 
   const uint64_t blocks = (chunks + kOpsThreads - 1) / kOpsThreads;
   hipLaunchKernelGGL(translate_kernel, dim3((uint32_t)blocks), dim3(kOpsThreads), 0, s, in, off, n,
                      frames, strands, pep_off, total_pep, lut, out);
+}
+
+void launch_codon_symbols(const uint8_t* in, uint64_t n_codons, const uint8_t* cls, uint32_t K,
+                          const uint8_t* lut, uint8_t* out, hipStream_t s) {
+  if (n_codons == 0) return;
+  const uint64_t blocks = (n_codons + 255) / 256;
+  hipLaunchKernelGGL(codon_symbols_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, in, n_codons,
+                     cls, K, lut, out);
 }
 
 }  // namespace magot

@@ -658,6 +658,21 @@ class Orf6Plan(object):
             pass
 
 
+def codon_symbols(seq, class256, n_classes, lut, ctx=None):
+    """One symbol per full codon of ``seq`` (str/bytes, length a multiple of 3)
+    over an extended alphabet (magot_codon_symbols): a list of ints."""
+    ctx = ctx or _lib.default_context()
+    buf = np.frombuffer(_as_bytes(seq), dtype=np.uint8)
+    m = len(buf) // 3
+    out = np.empty(max(m, 1), dtype=np.uint8)
+    cls = np.ascontiguousarray(class256, dtype=np.uint8)
+    lt = np.ascontiguousarray(lut, dtype=np.uint8)
+    check(_lib.lib().magot_codon_symbols(ctx.handle, ptr(buf) if m else None, m, ptr(cls),
+                                         int(n_classes), ptr(lt), ptr(out)),
+          'magot_codon_symbols')
+    return out[:m].tolist()
+
+
 def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
     """Untrimmed Sequence.translate (genome.py:795-822) residues per input, or None
     where the reference returns None.  The caller applies trimX."""
@@ -690,6 +705,7 @@ def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
     return res
 
 
-__all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'OUT_NUC',
+__all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'codon_symbols',
+           'OUT_NUC',
            'OUT_PEP', 'MagotError', 'GffPlan', 'orf6_batch', 'Orf6Plan', 'fasta_read',
            'FastaGenome', 'PartitionedGenome', 'device_genome', 'extract_records', 'plan_parts']

@@ -134,25 +134,120 @@ def ensure_file(potential_file):
 _ACGT = 'ACGT'
 
 
+def _ascii_upper(t):
+    """str.upper() of a Python 2 byte string: only a-z change."""
+    return t.translate(_UPPER)
+
+
+_UPPER = {c: c - 32 for c in range(ord('a'), ord('z') + 1)}
+
+
+def _matchable(key):
+    """Can ``key`` equal a triplet the reference's loop builds (1-3 upper-cased
+    characters, genome.py:810-812)?"""
+    return isinstance(key, str) and 1 <= len(key) <= 3 and _ascii_upper(key) == key
+
+
 def _library_lut(library):
-    """64-entry residue table (index c0 + 4*c1 + 16*c2) for a codon library,
-    or None for the standard code.  Libraries whose other keys could match an
-    upper-cased triplet, or with multi-character values, are not supported on
-    the device path."""
+    """64-entry residue table (index c0 + 4*c1 + 16*c2) for a codon library
+    that the standard translation kernel can run: every matchable key an ACGT
+    triplet with a one-character value.  None for the standard code; False
+    when the library needs the extended-alphabet path (_translate_general)."""
     if library is None or library is Sequence._STANDARD:
         return None
     lut = bytearray(b'X' * 64)
-    seen = 0
     for key, val in library.items():
-        if not (isinstance(val, str) and len(val) == 1):
-            raise NotImplementedError('codon library values must be single characters')
-        if isinstance(key, str) and len(key) == 3 and all(c in _ACGT for c in key):
-            x = _ACGT.index(key[0]) + 4 * _ACGT.index(key[1]) + 16 * _ACGT.index(key[2])
-            lut[x] = ord(val) & 0xFF
-            seen += 1
-        elif isinstance(key, str) and key == key.upper() and 1 <= len(key) <= 3:
-            raise NotImplementedError('codon library key %r is not an ACGT triplet' % key)
+        if not _matchable(key):
+            continue
+        if len(key) != 3 or any(c not in _ACGT for c in key):
+            return False
+        if not (isinstance(val, str) and len(val) == 1 and ord(val) < 256):
+            return False
+        x = _ACGT.index(key[0]) + 4 * _ACGT.index(key[1]) + 16 * _ACGT.index(key[2])
+        lut[x] = ord(val)
     return bytes(lut)
+
+
+def _lookup(library, triplet):
+    """``library[triplet]``, 'X' on KeyError (genome.py:813-816)."""
+    try:
+        return library[triplet]
+    except KeyError:
+        return 'X'
+
+
+def _translate_general(s, library, frame, strand, trimX):
+    """Sequence.translate (genome.py:795-822) for any library and any integer
+    frame.  The characters the loop visits -- positions frame .. len-1, a
+    negative position p reading seq[p] -- are laid out as one string V; its
+    first codon (1-3 characters: emitted where (p + frame) % 3 == 2) is looked
+    up here, every full codon after it on the GPU (magot_codon_symbols, an
+    extended-alphabet codon table), and the symbols mapped to the library's
+    values."""
+    n = len(s)
+    seq = s if strand == '+' else engine.revcomp_batch([s])[0]
+    if not (len(seq) > (2 + frame)):
+        return None
+    if not isinstance(frame, int):
+        raise TypeError('range() integer start argument expected, got %s.' % type(frame).__name__)
+    if frame < 0:
+        if -frame > n:
+            raise IndexError('string index out of range')
+        V = seq[frame:] + seq
+    else:
+        V = seq[frame:]
+    J = (2 - 2 * frame) % 3 + 1        # first emission at V position J - 1
+    first = _lookup(library, _ascii_upper(V[:J]))
+    body = V[J:]
+    m = len(body) // 3
+    # extended alphabet: ACGT, the other characters of matchable 3-char keys, other
+    chars = list(_ACGT)
+    for key in library.keys():
+        if _matchable(key) and len(key) == 3:
+            for c in key:
+                if c not in chars:
+                    chars.append(c)
+    K = len(chars) + 1
+    if K ** 3 > 32768:
+        raise NotImplementedError('codon library keys use more than 31 distinct characters')
+    cls = np.full(256, K - 1, dtype=np.uint8)
+    for i, c in enumerate(chars):
+        if ord(c) < 256:
+            cls[ord(c)] = i
+    for b in range(ord('a'), ord('z') + 1):
+        cls[b] = cls[b - 32]
+    values, lut = [], np.zeros(K ** 3, dtype=np.uint8)
+    for x in range(K ** 3):
+        c0, c1, c2 = x % K, (x // K) % K, x // (K * K)
+        if K - 1 in (c0, c1, c2):
+            v = 'X'                                    # no key holds this character
+        else:
+            v = _lookup(library, chars[c0] + chars[c1] + chars[c2])
+        for j, u in enumerate(values):
+            if u is v or (type(u) is type(v) and u == v):
+                break
+        else:
+            if len(values) == 256:
+                raise NotImplementedError('codon library has more than 256 distinct values')
+            values.append(v)
+            j = len(values) - 1
+        lut[x] = j
+    sym = engine.codon_symbols(V[J:J + 3 * m], cls, K, lut)
+    if not isinstance(first, str):
+        raise TypeError('can only concatenate str (not "%s") to str' % type(first).__name__)
+    for j in sorted(set(sym), key=sym.index):   # the first non-string value in order
+        if not isinstance(values[j], str):
+            raise TypeError('can only concatenate str (not "%s") to str'
+                            % type(values[j]).__name__)
+    if all(isinstance(v, str) and len(v) == 1 and ord(v) < 256 for v in values):
+        table = bytes(ord(v) for v in values) + bytes(256 - len(values))
+        newseq = first + bytes(sym).translate(table).decode('latin-1')
+    else:
+        newseq = first + ''.join([values[j] for j in sym])
+    if trimX:
+        if newseq[0] == 'X':
+            newseq = newseq[1:]
+    return newseq
 
 
 class Sequence(str):
@@ -166,12 +261,18 @@ class Sequence(str):
         return Sequence(engine.revcomp_batch([str(self)])[0])
 
     def translate(self, library=None, frame=0, strand='+', trimX=True):
-        """genome.py:795-822."""
+        """genome.py:795-822.  ``library=None`` is the reference's default
+        (standard) table.  Libraries of one-character values over ACGT
+        triplets and frames >= 0 run the batch translation kernel; any other
+        library (keys such as 'NNN' or 1-2 character keys matching the junk
+        codon, multi-character or non-string values) or a negative frame runs
+        _translate_general (extended-alphabet codon kernel)."""
         if strand not in ('+', '-'):
             raise UnboundLocalError("local variable 'seq' referenced before assignment")
-        if not isinstance(frame, int) or frame < 0:
-            raise NotImplementedError('negative or non-integer frames are not supported')
         lut = _library_lut(library)
+        if lut is False or not isinstance(frame, int) or frame < 0:
+            lib = Sequence._STANDARD if library is None else library
+            return _translate_general(str(self), lib, frame, strand, trimX)
         res = engine.translate_batch([str(self)], [frame], [strand], lut64=lut)[0]
         return _trim(res, trimX)
 
@@ -330,8 +431,8 @@ class _Batch(object):
     """Interval lists of every record of one get_fasta call."""
 
     def __init__(self):
-        self.seqdict = None
-        self.genome = None
+        self.genomes = []      # [(GenomeSequence, device genome)], in first-use order
+        self.ex_gid = []       # genome of each interval
         self.ex_start = []
         self.ex_contig = []
         self.ex_len = []
@@ -341,23 +442,56 @@ class _Batch(object):
         self.results = None
 
     def bind(self, seqdict):
-        if self.seqdict is None:
-            self.seqdict = seqdict
-            self.genome = _device_genome_for(seqdict)
-        elif seqdict is not self.seqdict:
-            raise NotImplementedError('one get_fasta call spans two genome sequences')
-        return self.genome
+        """(device genome, genome id) of a GenomeSequence.  One call usually
+        sees one genome; annotations of several (their annotation sets bound
+        to different Genomes) are gathered per genome in run()."""
+        for gid, (sd, dev) in enumerate(self.genomes):
+            if sd is seqdict:
+                return dev, gid
+        dev = _device_genome_for(seqdict)
+        self.genomes.append((seqdict, dev))
+        return dev, len(self.genomes) - 1
 
     def add(self, exons, kind):
-        """exons: list of (contig_index, start, length, rc)."""
+        """exons: list of (contig_index, start, length, rc, genome id)."""
         self.tx_begin.append(len(self.ex_start))
         self.tx_n.append(len(exons))
-        for ci, st, ln, rc in exons:
+        for ci, st, ln, rc, gid in exons:
             self.ex_start.append(st | (1 << 63) if rc else st)
             self.ex_contig.append(ci)
             self.ex_len.append(ln)
+            self.ex_gid.append(gid)
         self.kinds.append(kind)
         return len(self.kinds) - 1
+
+    def _run_genomes(self, ex, tx):
+        """Records over several genomes: each genome's intervals gathered as
+        one-interval pieces in one launch per genome, joined per record, and
+        the protein records translated in one translate_batch launch."""
+        gid = np.array(self.ex_gid, dtype=np.int64)
+        piece = [None] * len(ex)
+        for k, (_, dev) in enumerate(self.genomes):
+            idx = np.nonzero(gid == k)[0]
+            if len(idx) == 0:
+                continue
+            sub_tx = np.zeros(len(idx), dtype=engine.TX_DTYPE)
+            sub_tx['exon_begin'] = np.arange(len(idx), dtype=np.uint64)
+            sub_tx['n_exons'] = 1
+            nuc, noff, _, _ = engine.extract_records(dev, ex[idx], sub_tx, engine.OUT_NUC)
+            raw = nuc.tobytes().decode('latin-1') if nuc is not None else ''
+            for j, e in enumerate(idx.tolist()):
+                piece[e] = raw[int(noff[j]):int(noff[j + 1])]
+        recs = []
+        for b, n in zip(self.tx_begin, self.tx_n):
+            recs.append(''.join(piece[b:b + n]))
+        pep_ids = [i for i, k in enumerate(self.kinds) if k == 'pep']
+        res = list(recs)
+        if pep_ids:
+            peps = engine.translate_batch([recs[i] for i in pep_ids], [0] * len(pep_ids),
+                                          ['+'] * len(pep_ids))
+            for i, t in zip(pep_ids, peps):
+                res[i] = t or ''
+        return res
 
     def run(self):
         n = len(self.kinds)
@@ -371,25 +505,31 @@ class _Batch(object):
         tx = np.zeros(n, dtype=engine.TX_DTYPE)
         tx['exon_begin'] = np.array(self.tx_begin, dtype=np.uint64)
         tx['n_exons'] = np.array(self.tx_n, dtype=np.uint32)
-        outputs = 0
-        if 'nuc' in self.kinds:
-            outputs |= engine.OUT_NUC
-        if 'pep' in self.kinds:
-            outputs |= engine.OUT_PEP
-        nuc, noff, pep, poff = engine.extract_records(self.genome, ex, tx, outputs)
-        nraw = nuc.tobytes().decode('latin-1') if nuc is not None else ''
-        praw = pep.tobytes().decode('latin-1') if pep is not None else ''
-        noff = noff.tolist()
-        poff = poff.tolist()
-        res = []
+        if not self.genomes:      # no record has an interval: every sequence is empty
+            res = [''] * n
+        elif len(self.genomes) > 1:
+            res = self._run_genomes(ex, tx)
+        else:
+            outputs = 0
+            if 'nuc' in self.kinds:
+                outputs |= engine.OUT_NUC
+            if 'pep' in self.kinds:
+                outputs |= engine.OUT_PEP
+            genome = self.genomes[0][1] if self.genomes else None
+            nuc, noff, pep, poff = engine.extract_records(genome, ex, tx, outputs)
+            nraw = nuc.tobytes().decode('latin-1') if nuc is not None else ''
+            praw = pep.tobytes().decode('latin-1') if pep is not None else ''
+            noff = noff.tolist()
+            poff = poff.tolist()
+            res = []
+            for i, kind in enumerate(self.kinds):
+                if kind == 'nuc':
+                    res.append(nraw[noff[i]:noff[i + 1]])
+                else:
+                    res.append(praw[poff[i]:poff[i + 1]])
         for i, kind in enumerate(self.kinds):
-            if kind == 'nuc':
-                res.append(nraw[noff[i]:noff[i + 1]])
-            else:
-                s = praw[poff[i]:poff[i + 1]]
-                if s and s[0] == 'X':     # trimX (genome.py:819-821)
-                    s = s[1:]
-                res.append(s)
+            if kind == 'pep' and res[i] and res[i][0] == 'X':  # trimX (genome.py:819-821)
+                res[i] = res[i][1:]
         self.results = res
 
     def render(self, node):
@@ -530,8 +670,8 @@ class BaseAnnotation(object):
             seqs = self.annotation_set.genome.genome_sequence
             contig = seqs[self.seqid]
             start, length = _slice_interval(contig, self.coords[0] - 1, self.coords[1])
-            dev = batch.bind(seqs)
-            return (dev.index[self.seqid], start, length, rc)
+            dev, gid = batch.bind(seqs)
+            return (dev.index[self.seqid], start, length, rc, gid)
         except (NotImplementedError, engine.MagotError):
             raise  # device / build failures are not reference semantics: fail loudly
         except Exception:
@@ -595,8 +735,8 @@ class ParentAnnotation(object):
                 contig = seqs[self.seqid]
                 head = '>' + self.ID + '\n'
                 start, length = _slice_interval(contig, span[0] - 1, span[1])
-                dev = batch.bind(seqs)
-                job = batch.add([(dev.index[self.seqid], start, length, False)], 'nuc')
+                dev, gid = batch.bind(seqs)
+                job = batch.add([(dev.index[self.seqid], start, length, False, gid)], 'nuc')
                 return _Cat([head, _Rec(job), '\n'])
             return None
         if not (len(self.child_list) > 0 and aset is not None):

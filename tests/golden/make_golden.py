@@ -18,6 +18,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   orfs.json       dna2orfs output files (six-frame ORFs of whole contigs)
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
+  translate_lib.json Sequence.translate with non-standard libraries, frames -6..6
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -109,6 +110,51 @@ def make_kat(ref):
                 rec['orfs']['%d%d' % (int(longest), int(atg))] = {'exc': e} if e else r
         out.append(rec)
     return out
+
+
+# Codon libraries beyond the standard table (Sequence.translate's `library`,
+# genome.py:795-818): keys that are not ACGT triplets ('NNN', IUPAC, the 1-
+# and 2-character junk codons of frames 1/2), multi-character, empty and
+# non-string values, lower-case keys that never match; frames -6..6.
+TRANSLATE_LIBS = {
+    'std+junk': ('standard', {'NNN': 'Z', 'A': 'a', 'AC': 'b', 'RYK': 'r', 'N-.': '#',
+                              'ATGC': 'never'}),
+    'multi': ('standard', {'ATG': 'Met', 'TAA': '', 'TAG': 'Stop', 'TGA': '*', 'GCC': 'XA'}),
+    'sparse': (None, {'ATG': 'M', 'AAA': 'K', 'NNN': 'n', 'atg': 'lower', 'T': 'j'}),
+    'intval': (None, {'ATG': 5, 'CCC': 'P'}),
+    'empties': (None, {'ATG': '', 'CCC': '', 'GGG': 'G', 'TTT': ''}),
+    'X-lead': ('standard', {'ATG': 'XM', 'GCC': 'X'}),
+}
+
+
+def translate_library(name, std):
+    base, extra = TRANSLATE_LIBS[name]
+    lib = dict(std) if base == 'standard' else {}
+    lib.update(extra)
+    return lib
+
+
+def make_translate_lib(ref):
+    std = ref.Sequence.translate.__defaults__[0]
+    rnd = random.Random(1017)
+    alpha = 'ACGTACGTACGTacgtNnRYKMSW-.*'
+    strs = list(KAT_STRINGS)
+    for n in (0, 1, 2, 3, 4, 5, 6, 7, 8, 11, 13, 20, 31, 40):
+        for _ in range(2):
+            strs.append(''.join(rnd.choice(alpha) for _ in range(n)))
+    out = []
+    for name in sorted(TRANSLATE_LIBS):
+        lib = translate_library(name, std)
+        for s in strs:
+            S = ref.Sequence(s)
+            for frame in range(-6, 7):
+                for strand in '+-':
+                    for trim in (True, False):
+                        r, e, _ = call(lambda: S.translate(library=lib, frame=frame,
+                                                           strand=strand, trimX=trim))
+                        out.append({'lib': name, 'seq': s, 'frame': frame, 'strand': strand,
+                                    'trim': trim, 'out': None if e else r, 'exc': e})
+    return {'libs': {k: [v[0], v[1]] for k, v in TRANSLATE_LIBS.items()}, 'cases': out}
 
 
 # ---------------------------------------------------------------------------
@@ -686,6 +732,10 @@ def make_cds2pep(ref_tools, n=40):
 
 def main():
     ref = reference_module()
+    with open(os.path.join(HERE, 'translate_lib.json'), 'w') as fh:
+        json.dump(make_translate_lib(ref), fh, indent=0, sort_keys=True)
+    if '--only-translate-lib' in sys.argv:
+        return
     with open(os.path.join(HERE, 'fuzz.json'), 'w') as fh:
         json.dump(make_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'fuzz2.json'), 'w') as fh:

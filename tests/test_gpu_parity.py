@@ -124,6 +124,42 @@ def test_get_seq_single_interval():
     assert s == 'nnNNaaccggT' and isinstance(s, G.Sequence)
 
 
+@pytest.mark.parametrize('seq_type', ['nucleotide', 'protein'])
+def test_get_fasta_children_from_two_genomes(seq_type):
+    """A record whose children belong to annotation sets of two Genomes (CDS
+    objects grafted from one set into another keep their own
+    annotation_set, so get_seq reads their own genome, genome.py:603-608):
+    one launch per genome, joined per record; against the oracle's object
+    model built the same way."""
+    fa1 = 'ACGTACGTAAccggttNNRYacgtACGTAAATTTGGGCCC'
+    fa2 = {'c1': 'TTTTGGGGCCCCAAAATGATGATGCCCGGGAAATTT', 'c9': 'ATGCCCtagGGA'}
+    g1 = G.Genome('>c1\n%s\n' % fa1)
+    g1.read_gff('c1\tt\tgene\t1\t40\t.\t+\t.\tID=g\n'
+                'c1\tt\tmRNA\t1\t40\t.\t+\t.\tID=t;Parent=g\n'
+                'c1\tt\tCDS\t1\t6\t.\t+\t0\tID=a1;Parent=t\n'
+                'c1\tt\tCDS\t10\t20\t.\t+\t0\tID=a2;Parent=t\n')
+    g2 = G.Genome('>c1\n%s\n>c9\n%s\n' % (fa2['c1'], fa2['c9']))
+    g2.read_gff('c1\tt\tgene\t1\t30\t.\t+\t.\tID=h\n'
+                'c1\tt\tmRNA\t1\t30\t.\t+\t.\tID=u;Parent=h\n'
+                'c1\tt\tCDS\t22\t27\t.\t+\t0\tID=b1;Parent=u\n'
+                'c9\tt\tCDS\t1\t9\t.\t+\t0\tID=b2;Parent=u\n')
+    s1 = g1.annotations
+    for cid in ('b1', 'b2'):
+        s1.CDS[cid] = g2.annotations.CDS[cid]
+        s1.mRNA['t'].child_list.append(cid)
+    got = s1.mRNA['t'].get_fasta(seq_type=seq_type)
+
+    o1 = mo.OracleSet(mo.OracleGenome({'c1': fa1}))
+    o2 = mo.OracleSet(mo.OracleGenome(fa2))
+    kids = [('a1', 'c1', (1, 6), o1), ('a2', 'c1', (10, 20), o1), ('b1', 'c1', (22, 27), o2),
+            ('b2', 'c9', (1, 9), o2)]
+    for cid, sid, co, owner in kids:
+        o1.CDS[cid] = mo.OBase(cid, sid, co, 'CDS', 't', '+', {}, owner)
+    o1.mRNA = {'t': mo.OParent('t', 'c1', 'mRNA', [k[0] for k in kids], 'g', '+', o1, {})}
+    want = mo.get_fasta(o1.mRNA['t'], o1, seq_type)
+    assert got == want and want.count('\n') == 1
+
+
 def _gff2fasta(fasta, gff, **kw):
     order = kw.pop('order', 'insertion')
     g = G.Genome(fasta)

@@ -33,7 +33,8 @@ def _oracle_run(self):
             st = self.ex_start[e]
             rc = bool(st >> 63)
             st &= (1 << 63) - 1
-            s = self.genome.seqs[self.ex_contig[e]][st:st + self.ex_len[e]]
+            dev = self.genomes[self.ex_gid[e]][1]
+            s = dev.seqs[self.ex_contig[e]][st:st + self.ex_len[e]]
             parts.append(mo.reverse_complement(s) if rc else s)
         s = ''.join(parts)
         res.append(s if kind == 'nuc' else mo.translate(s))
