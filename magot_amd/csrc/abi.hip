@@ -814,12 +814,16 @@ uint64_t magot_plan_algorithmic_bytes(const magot_plan* p) {
 int magot_revcomp_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
                         uint8_t* out) {
   if (int rc = bind(ctx)) return rc;
-  if (!seq_off || (n && (!seqs || !out))) {
+  if (!seq_off) {
     set_error("magot_revcomp_batch: null argument");
     return MAGOT_ERR_ARG;
   }
   const uint64_t total = n ? seq_off[n] : 0;
-  if (total == 0) return MAGOT_OK;
+  if (total == 0) return MAGOT_OK;  // empty strings only: nothing to read or write
+  if (!seqs || !out) {
+    set_error("magot_revcomp_batch: null argument");
+    return MAGOT_ERR_ARG;
+  }
   for (uint64_t i = 0; i < n; ++i)
     if (seq_off[i + 1] < seq_off[i]) {
       set_error("magot_revcomp_batch: offsets not monotone");
