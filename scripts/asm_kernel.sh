@@ -7,7 +7,7 @@ SRC=$1; SYM=$2; OUT=${3:-/tmp/asm}
 mkdir -p $OUT
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 base=$(basename $SRC .hip)
-timeout 300 /opt/rocm/bin/hipcc -O3 -std=c++17 -I$ROOT/include --offload-arch=gfx950 -x hip \
+timeout 300 /opt/rocm/bin/hipcc $EXTRA -O3 -std=c++17 -I$ROOT/include --offload-arch=gfx950 -x hip \
   --cuda-device-only -S $SRC -o $OUT/$base.s 2>&1 | grep -v hip-link
 s=$(grep -n "^${SYM}" $OUT/$base.s | head -1 | cut -d: -f1)
 e=$(awk -v s=$s 'NR>s && /^\.Lfunc_end/ {print NR; exit}' $OUT/$base.s)
