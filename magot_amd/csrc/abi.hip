@@ -553,46 +553,65 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   };
   std::vector<uint64_t> tile_start, tile_q;
   std::vector<uint32_t> tile_ex, tile_tx;
-  uint64_t e1 = 0, e2 = 0;
-  uint64_t T0 = 0, R0 = 0;
-  while (T0 < B) {
-    while (e1 < Ec && ex_out[e1 + 1] <= T0) ++e1;           // interval containing T0
-    const uint64_t j1 = R0 < P ? rec_of(R0) : Tc;            // record holding residue R0
-    uint64_t T1 = std::min<uint64_t>(T0 + kTile, B);
-    if (e1 + kExonCap < Ec) T1 = std::min<uint64_t>(T1, ex_out[e1 + kExonCap] - kHalo);
-    if (j1 + kTxCap - kChunk < Tc) T1 = std::min<uint64_t>(T1, tn[j1 + kTxCap - kChunk]);
-    if (T1 < B) T1 &= ~(uint64_t)(kChunk - 1);
-    if (T1 < T0 + kChunk) T1 = std::min<uint64_t>(T0 + kChunk, B);
-    const uint64_t dec_end = std::min<uint64_t>(T1 + kHalo, B);
-    // residues owned: every codon starting before T1, rounded up to a chunk,
-    // but only codons that end inside the decoded range and at most kPepSlots chunks
-    uint64_t R1 = P;
-    if (T1 < B) {
-      R1 = std::min<uint64_t>((pcount(T1) + kChunk - 1) & ~(uint64_t)(kChunk - 1), P);
-      R1 = std::min<uint64_t>(R1, pcount(dec_end - 2));
-      R1 = std::min<uint64_t>(R1, (R0 & ~(uint64_t)(kChunk - 1)) + kPepSlots * kChunk);
+  // cut the output into tiles of at most `tile` bytes (see tile_bytes)
+  auto cut = [&](uint64_t tile) -> int {
+    tile_start.clear();
+    tile_q.clear();
+    tile_ex.clear();
+    tile_tx.clear();
+    uint64_t e1 = 0, e2 = 0;
+    uint64_t T0 = 0, R0 = 0;
+    while (T0 < B) {
+      while (e1 < Ec && ex_out[e1 + 1] <= T0) ++e1;           // interval containing T0
+      const uint64_t j1 = R0 < P ? rec_of(R0) : Tc;            // record holding residue R0
+      uint64_t T1 = std::min<uint64_t>(T0 + tile, B);
+      if (e1 + kExonCap < Ec) T1 = std::min<uint64_t>(T1, ex_out[e1 + kExonCap] - kHalo);
+      if (j1 + kTxCap - kChunk < Tc) T1 = std::min<uint64_t>(T1, tn[j1 + kTxCap - kChunk]);
+      if (T1 < B) T1 &= ~(uint64_t)(kChunk - 1);
+      if (T1 < T0 + kChunk) T1 = std::min<uint64_t>(T0 + kChunk, B);
+      const uint64_t dec_end = std::min<uint64_t>(T1 + kHalo, B);
+      // residues owned: every codon starting before T1, rounded up to a chunk,
+      // but only codons that end inside the decoded range and at most kPepSlots chunks
+      uint64_t R1 = P;
+      if (T1 < B) {
+        R1 = std::min<uint64_t>((pcount(T1) + kChunk - 1) & ~(uint64_t)(kChunk - 1), P);
+        R1 = std::min<uint64_t>(R1, pcount(dec_end - 2));
+        R1 = std::min<uint64_t>(R1, (R0 & ~(uint64_t)(kChunk - 1)) + kPepSlots * kChunk);
+      }
+      if (R1 < R0) R1 = R0;
+      if (e2 < e1) e2 = e1;
+      while (e2 < Ec && ex_out[e2] < dec_end) ++e2;           // intervals touching the decode range
+      const uint64_t j2 = R1 > R0 ? rec_of(R1 - 1) + 1 : j1;  // records holding residues [R0, R1)
+      if (e2 - e1 > (uint64_t)kExonCap || (R1 > R0 && j2 - j1 > (uint64_t)kTxCap) ||
+          (R1 > R0 && tn[rec_of(R1 - 1)] + 3 * (R1 - 1 - tp[rec_of(R1 - 1)]) + 3 > dec_end)) {
+        set_error("magot_plan_create: internal tiling error");
+        return MAGOT_ERR_STATE;
+      }
+      tile_start.push_back(T0);
+      tile_q.push_back(R0);
+      tile_ex.push_back((uint32_t)e1);
+      tile_ex.push_back((uint32_t)e2);
+      tile_tx.push_back((uint32_t)(R1 > R0 ? j1 : 0));
+      tile_tx.push_back((uint32_t)(R1 > R0 ? j2 : 0));
+      T0 = T1;
+      R0 = R1;
     }
-    if (R1 < R0) R1 = R0;
-    if (e2 < e1) e2 = e1;
-    while (e2 < Ec && ex_out[e2] < dec_end) ++e2;           // intervals touching the decode range
-    const uint64_t j2 = R1 > R0 ? rec_of(R1 - 1) + 1 : j1;  // records holding residues [R0, R1)
-    if (e2 - e1 > (uint64_t)kExonCap || (R1 > R0 && j2 - j1 > (uint64_t)kTxCap) ||
-        (R1 > R0 && tn[rec_of(R1 - 1)] + 3 * (R1 - 1 - tp[rec_of(R1 - 1)]) + 3 > dec_end)) {
-      set_error("magot_plan_create: internal tiling error");
+    if (R0 != P) {
+      set_error("magot_plan_create: internal tiling error (residues)");
       return MAGOT_ERR_STATE;
     }
-    tile_start.push_back(T0);
-    tile_q.push_back(R0);
-    tile_ex.push_back((uint32_t)e1);
-    tile_ex.push_back((uint32_t)e2);
-    tile_tx.push_back((uint32_t)(R1 > R0 ? j1 : 0));
-    tile_tx.push_back((uint32_t)(R1 > R0 ? j2 : 0));
-    T0 = T1;
-    R0 = R1;
-  }
-  if (R0 != P) {
-    set_error("magot_plan_create: internal tiling error (residues)");
-    return MAGOT_ERR_STATE;
+    return MAGOT_OK;
+  };
+  // the large tile, or the small one for plans too small to fill the chip
+  // several times over (MAGOT_EXTRACT_LANE_CHUNKS=3|5 forces one, for A/Bs)
+  uint32_t lane_chunks = kLaneChunksLarge;
+  if (int rc = cut(tile_bytes(kLaneChunksLarge))) return rc;
+  const char* lc_env = std::getenv("MAGOT_EXTRACT_LANE_CHUNKS");
+  const int lc_force = lc_env ? std::atoi(lc_env) : 0;
+  if (lc_force == kLaneChunksSmall ||
+      (lc_force != kLaneChunksLarge && tile_start.size() < kSmallTilePlan)) {
+    lane_chunks = kLaneChunksSmall;
+    if (int rc = cut(tile_bytes(kLaneChunksSmall))) return rc;
   }
   tile_start.push_back(B);
   tile_q.push_back(P);
@@ -658,6 +677,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   a.total_pep = P;
   a.n_tiles = n_tiles;
   a.outputs = outputs;
+  a.lane_chunks = lane_chunks;
   if (const char* dbg = std::getenv("MAGOT_DEBUG_PATHS")) {
     const int v = std::atoi(dbg);
     if (v & 1) a.outputs |= kDebugSlowNuc;

@@ -81,13 +81,18 @@ void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out);
 constexpr int kThreads = 256;                 // one workgroup = 4 independent waves
 constexpr int kWaves = kThreads / 64;
 constexpr int kChunk = 16;                    // bytes per lane-store
-#ifndef MAGOT_EXP_LANE_CHUNKS
-#define MAGOT_EXP_LANE_CHUNKS 5
-#endif
-constexpr int kLaneChunks = MAGOT_EXP_LANE_CHUNKS;  // chunk slots per lane per tile
-constexpr int kSlots = 64 * kLaneChunks;      // 320 chunk slots per wave tile
-constexpr int kTile = (kSlots - 3) * kChunk;  // 5072 output bytes per tile (3 slots of halo):
-                                              // <= 1691 residues, <= 106 residue chunks
+// Chunk slots per lane per tile: 5 (5072-byte tiles) for large plans; 3
+// (3024-byte tiles) for plans too small to fill the chip several times over,
+// where the launch tail dominates (one GPU's share of an 8-GPU C4 job: -3.5 %
+// per launch, A/B in DESIGN.md; at full C3 size 4 slots are +3.6 % slower).
+constexpr int kLaneChunksLarge = 5, kLaneChunksSmall = 3;
+constexpr int kLaneChunks = kLaneChunksLarge;   // the larger tile (LDS sizing, clamps)
+constexpr int kSlots = 64 * kLaneChunks;        // 320 chunk slots per wave tile
+constexpr int kTile = (kSlots - 3) * kChunk;    // 5072 output bytes per tile (3 slots of halo):
+                                                // <= 1691 residues, <= 106 residue chunks
+constexpr int tile_bytes(int lane_chunks) { return (64 * lane_chunks - 3) * 16; }
+// plans whose large-tile count is below this use the small tile
+constexpr uint64_t kSmallTilePlan = 40000;
 constexpr int kPepPerLane = 2;                // residue chunk slots per lane
 constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
                                               // the residues rounded up to a 16-byte store
@@ -161,6 +166,7 @@ struct ExtractArgs {
   uint32_t n_tiles;
   uint32_t outputs;
   uint32_t lut[16];           // 64 residue bytes indexed c0 + 4*c1 + 16*c2
+  uint32_t lane_chunks;       // tile size the plan was cut for (kLaneChunksLarge / Small)
 };
 
 // Wave-wide inclusive prefix sum with DPP row shifts and row broadcasts

@@ -42,14 +42,17 @@ namespace {
 
 constexpr int kGuard = 4;  // LDS words before codes[0] (codons of residue chunk 0 may start < 0)
 
+template <int LC>
 struct WaveLds {
+  static constexpr int kS = 64 * LC;      // chunk slots
   uint4 ex[kExonCap];                     // {plane byte offset, anchor lo, end (tile-rel), flags}
   uint32_t vb[kExonCap];                  // reverse-forward rows: forward-plane byte offset
   int64_t tn[kTxCap + 1];                 // record codon-0 output position, tile-relative
   int64_t tp[kTxCap + 1];                 // record first residue, relative to the tile's Q0
-  uint32_t codes_g[kGuard + kSlots + 8];  // 2-bit codes per chunk (histogram scratch first)
-  uint32_t valid_g[kGuard + kSlots / 2 + 8];  // 16 validity bits per chunk (scratch first)
-  uint8_t cmap[kSlots];                   // chunk slot -> interval
+  uint32_t codes_g[kGuard + kS + 8];      // 2-bit codes per chunk (histogram scratch first)
+  uint32_t valid_g[kGuard + (kS > 2 * kPepSlots ? kS : 2 * kPepSlots) / 2 + 8];  // 16 validity
+                                          // bits per chunk (residue-chunk histogram first)
+  uint8_t cmap[kS];                       // chunk slot -> interval
   uint8_t pmap[kPepSlots];                // residue chunk -> record
 };
 
@@ -346,12 +349,13 @@ __device__ __forceinline__ TileGeom geom(const ExtractArgs& a, const TileDesc& d
 // Stage one tile into the wave's LDS: interval rows {anchor, end, flags},
 // record rows, and the chunk->interval / residue chunk->record maps
 // (histogram of first chunks + wave prefix scan).
-__device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* valid32,
+template <int LC>
+__device__ __forceinline__ void stage(WaveLds<LC>& L, uint32_t* codes, uint32_t* valid32,
                                       const TileDesc& d, const TileGeom& g, const TileRows& rows,
                                       uint64_t span, int lane) {
   const int m = (int)d.m, nt = (int)d.nt;
 #pragma unroll
-  for (int h = 0; h < kLaneChunks; ++h) codes[lane + 64 * h] = 0;
+  for (int h = 0; h < LC; ++h) codes[lane + 64 * h] = 0;
 #pragma unroll
   for (int h = 0; h < kPepPerLane; ++h) valid32[lane + 64 * h] = 0;
   __builtin_amdgcn_wave_barrier();
@@ -363,7 +367,7 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
       const int64_t s = (int64_t)(o0 - d.T0);
       const int64_t e = (int64_t)(o1 - d.T0);
       const uint64_t U = row_anchor(gw, o0, o1, d.T0, span);
-      const uint32_t end32 = (uint32_t)min(e, (int64_t)(kTile + 4 * kHalo));
+      const uint32_t end32 = (uint32_t)min(e, (int64_t)(tile_bytes(LC) + 4 * kHalo));
       // reverse-forward: chunk c's 16 bytes are the forward bases V - 16c ..
       // V - 16c + 15, reversed and complemented (V = gs + len - 16 + s)
       const bool revfwd = (gw & kRcBit) && !(gw & kExcBit);
@@ -396,20 +400,20 @@ __device__ __forceinline__ void stage(WaveLds& L, uint32_t* codes, uint32_t* val
     }
   }
   __builtin_amdgcn_wave_barrier();
-  // lane l scans chunk slots kLaneChunks*l .. and residue chunks
+  // lane l scans chunk slots LC*l .. and residue chunks
   // kPepPerLane*l .. (inclusive running counts)
-  uint32_t hc[kLaneChunks], pc[kPepPerLane];
+  uint32_t hc[LC], pc[kPepPerLane];
 #pragma unroll
-  for (int i = 0; i < kLaneChunks; ++i) hc[i] = codes[kLaneChunks * lane + i] + (i ? hc[i - 1] : 0u);
+  for (int i = 0; i < LC; ++i) hc[i] = codes[LC * lane + i] + (i ? hc[i - 1] : 0u);
 #pragma unroll
   for (int i = 0; i < kPepPerLane; ++i) pc[i] = valid32[kPepPerLane * lane + i] + (i ? pc[i - 1] : 0u);
-  const uint32_t ct = hc[kLaneChunks - 1], pt = pc[kPepPerLane - 1];
+  const uint32_t ct = hc[LC - 1], pt = pc[kPepPerLane - 1];
   // both scans in one: interval counts (<= kExonCap) low, record counts high
   const uint32_t sc = wave_scan(ct | (pt << 16));
   const uint32_t cx = (sc & 0xFFFFu) - ct;
   const uint32_t px = (sc >> 16) - pt;
 #pragma unroll
-  for (int i = 0; i < kLaneChunks; ++i) L.cmap[kLaneChunks * lane + i] = (uint8_t)(cx + hc[i]);
+  for (int i = 0; i < LC; ++i) L.cmap[LC * lane + i] = (uint8_t)(cx + hc[i]);
 #pragma unroll
   for (int i = 0; i < kPepPerLane; ++i) L.pmap[kPepPerLane * lane + i] = (uint8_t)(px + pc[i]);
   __builtin_amdgcn_wave_barrier();
@@ -458,14 +462,15 @@ __device__ __forceinline__ void fast_chunk(uint3 A, uint3 B, uint32_t mt, const 
   x1 = bfi(m.y, a1, b1);
 }
 
+template <int LC>
 __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
-  __shared__ WaveLds s_wave[kWaves];
+  __shared__ WaveLds<LC> s_wave[kWaves];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[64];
   __shared__ uint2 s_mask[34];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  WaveLds& L = s_wave[wave];
+  WaveLds<LC>& L = s_wave[wave];
   uint32_t* const codes = L.codes_g + kGuard;
   uint32_t* const valid32 = L.valid_g + kGuard;
   uint16_t* const valid16 = reinterpret_cast<uint16_t*>(valid32);
@@ -519,11 +524,11 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
 
   // ---- nucleotide chunks: issue every window load first -------------------
   const __amdgpu_buffer_rsrc_t nib_rs = plane_rsrc(a.nib);
-  uint3 wA[kLaneChunks], wB[kLaneChunks];
-  uint32_t meta[kLaneChunks];  // bit0 active, 2 reversed, 4 slow, 8..10 / 16..18 nibble
+  uint3 wA[LC], wB[LC];
+  uint32_t meta[LC];  // bit0 active, 2 reversed, 4 slow, 8..10 / 16..18 nibble
                                // shift of the A / B window, 24..29 mask index
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) {
+  for (int k = 0; k < LC; ++k) {
     const int c = min(lane + 64 * k, g.n_all - 1);  // clamped: inactive lanes redo a chunk
     const int p = c * kChunk;
     const int i = L.cmap[c];
@@ -557,9 +562,9 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
     wA[k] = load_window(nib_rs, offa);
     wB[k] = load_window(nib_rs, offb);
   }
-  uint32_t x0k[kLaneChunks], x1k[kLaneChunks];
+  uint32_t x0k[LC], x1k[LC];
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) {
+  for (int k = 0; k < LC; ++k) {
     fast_chunk(wA[k], wB[k], meta[k], s_mask, x0k[k], x1k[k]);
     const uint32_t r0 = revcomp8(x1k[k]), r1 = revcomp8(x0k[k]);
     const bool rv = (meta[k] & 4u) != 0;
@@ -568,7 +573,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   }
   uint32_t slow_any = 0, exc_any = 0;
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) {
+  for (int k = 0; k < LC; ++k) {
     slow_any |= meta[k] & 16u;
     exc_any |= (meta[k] & 1u) ? (x0k[k] | x1k[k]) & 0x88888888u : 0u;
   }
@@ -577,7 +582,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   // the wave decodes them from the nibble, without the run list
   const bool any_exc = __builtin_amdgcn_readfirstlane(__ballot(exc_any != 0) != 0);
 #pragma unroll
-  for (int k = 0; k < kLaneChunks; ++k) {
+  for (int k = 0; k < LC; ++k) {
     const int c = lane + 64 * k;
     const int p = c * kChunk;
     const uint32_t mt = meta[k];
@@ -748,11 +753,12 @@ void launch_mirror_planes(uint32_t* nib, uint64_t span, hipStream_t s) {
 // overrides it (0: no cap).
 constexpr int kExtractBlocksPerCu = 6;
 
+template <int LC>
 size_t extract_lds_pad() {
   static const size_t pad = [] {
     const char* env = getenv("MAGOT_EXTRACT_BLOCKS_PER_CU");
     const int want = env ? atoi(env) : kExtractBlocksPerCu;
-    return occupancy_lds_pad(reinterpret_cast<const void*>(extract_kernel), kThreads, want);
+    return occupancy_lds_pad(reinterpret_cast<const void*>(extract_kernel<LC>), kThreads, want);
   }();
   return pad;
 }
@@ -760,13 +766,19 @@ size_t extract_lds_pad() {
 void launch_extract(const ExtractArgs& a, hipStream_t s) {
   if (a.n_tiles == 0) return;
   const uint32_t grid = (a.n_tiles + kWaves - 1) / kWaves;  // one tile per wave
-  hipLaunchKernelGGL(extract_kernel, dim3(grid), dim3(kThreads), extract_lds_pad(), s, a);
+  if (a.lane_chunks == kLaneChunksSmall)
+    hipLaunchKernelGGL(extract_kernel<kLaneChunksSmall>, dim3(grid), dim3(kThreads),
+                       extract_lds_pad<kLaneChunksSmall>(), s, a);
+  else
+    hipLaunchKernelGGL(extract_kernel<kLaneChunksLarge>, dim3(grid), dim3(kThreads),
+                       extract_lds_pad<kLaneChunksLarge>(), s, a);
 }
 
 int extract_blocks_per_cu() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extract_kernel, kThreads,
-                                                   extract_lds_pad()) != hipSuccess)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, extract_kernel<kLaneChunksLarge>, kThreads,
+                                                   extract_lds_pad<kLaneChunksLarge>()) !=
+      hipSuccess)
     return 0;
   return n;
 }

@@ -29,6 +29,18 @@ def _sha(s):
     return hashlib.sha256(s).hexdigest()
 
 
+@pytest.fixture(autouse=True, params=['auto', '5'])
+def tile_size(request, monkeypatch):
+    """Every test under both extraction tile sizes: 'auto' (test-size plans
+    take the small 3-slot tile, full-size ones the large tile) and the large
+    5-slot tile forced (magot_plan_create reads MAGOT_EXTRACT_LANE_CHUNKS)."""
+    if request.param == 'auto':
+        monkeypatch.delenv('MAGOT_EXTRACT_LANE_CHUNKS', raising=False)
+    else:
+        monkeypatch.setenv('MAGOT_EXTRACT_LANE_CHUNKS', request.param)
+    return request.param
+
+
 @pytest.fixture(scope='module', autouse=True)
 def _device():
     from magot_amd import _lib
