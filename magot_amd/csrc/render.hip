@@ -54,8 +54,10 @@ __global__ __launch_bounds__(256) void text_copy_kernel(
     const TextUnit* __restrict__ units, uint64_t n, const uint64_t* __restrict__ roff,
     const uint8_t* __restrict__ pay, int protein, const uint8_t* __restrict__ text,
     const uint64_t* __restrict__ end, uint8_t* __restrict__ out) {
-  const uint64_t w = __builtin_amdgcn_readfirstlane(
-      (uint64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave);
+  // wave index: readfirstlane takes 32 bits, so the (wave-uniform) block part
+  // stays 64-bit outside it (units may exceed 2^32 / 4 blocks)
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x / kWave) +
+                     (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   if (w >= n) return;
   const int lane = threadIdx.x % kWave;
   const TextUnit u = units[w];

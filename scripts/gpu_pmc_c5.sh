@@ -12,7 +12,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES" \
            "GRBM_GUI_ACTIVE SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS"; do
   i=$((i+1))
-  timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python bench.py --config C5 --steps 3 --warmup 1 --no-verify > $OUT/pmc$i.log 2>&1
+  timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python bench.py --config C5 --steps 3 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline > $OUT/pmc$i.log 2>&1
   rc=$?
   if [ $rc -ne 0 ]; then echo "pmc group $i failed rc=$rc"; tail -3 $OUT/pmc$i.log; [ $rc -ge 124 ] && exit 1; fi
 done
