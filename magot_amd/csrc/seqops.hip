@@ -200,34 +200,47 @@ __device__ __forceinline__ uint32_t funnel4(uint32_t hi, uint32_t lo, uint32_t s
   return __builtin_amdgcn_alignbit(hi, lo, sh);
 }
 
-// Eight nibbles (code | lower << 2 | exception << 3) -> two words of
-// e-bytes (code | exception << 6), one base per byte.
-__device__ __forceinline__ void nibbles_to_e(uint32_t x, uint32_t& e0, uint32_t& e1) {
-  const uint32_t lo = x & 0x0F0F0F0Fu;         // nibbles 0 2 4 6
-  const uint32_t hi = (x >> 4) & 0x0F0F0F0Fu;  // nibbles 1 3 5 7
-  const uint32_t s0 = __builtin_amdgcn_perm(hi, lo, 0x05010400u);
-  const uint32_t s1 = __builtin_amdgcn_perm(hi, lo, 0x07030602u);
-  e0 = (s0 & 0x03030303u) | ((s0 & 0x08080808u) << 3);
-  e1 = (s1 & 0x03030303u) | ((s1 & 0x08080808u) << 3);
+// Sixteen nibbles (code | lower << 2 | exception << 3, base k of x0:x1 at
+// nibble k) -> sixteen packed 2-bit codes (base k at bits 2k).
+__device__ __forceinline__ uint32_t nib_codes(uint32_t x0, uint32_t x1) {
+  const uint32_t y0 = (x0 & 0x03030303u) | ((x0 >> 2) & 0x0C0C0C0Cu);
+  const uint32_t y1 = (x1 & 0x03030303u) | ((x1 >> 2) & 0x0C0C0C0Cu);
+  const uint32_t z0 = (y0 & 0x0F0F0F0Fu) | ((y0 >> 4) & 0xF0F0F0F0u);
+  const uint32_t z1 = (y1 & 0x0F0F0F0Fu) | ((y1 >> 4) & 0xF0F0F0F0u);
+  return __builtin_amdgcn_perm(z1, z0, 0x06040200u);
 }
 
-// cidx bytes of 16 positions from their e-bytes and the next two.
-__device__ __forceinline__ uint4 codon_indices(const uint32_t e[5]) {
-  uint32_t o[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t e1 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 1);
-    const uint32_t e2 = __builtin_amdgcn_alignbyte(e[j + 1], e[j], 2);
-    o[j] = (e[j] & 0x03030303u) | ((e1 & 0x03030303u) << 2) | ((e2 & 0x03030303u) << 4) |
-           ((e[j] | e1 | e2) & 0x40404040u);
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
+// The exception bits (nibble bit 3) of sixteen nibbles as a 16-bit mask.
+__device__ __forceinline__ uint32_t nib_exc16(uint32_t x0, uint32_t x1) {
+  uint32_t e0 = (x0 >> 3) & 0x11111111u, e1 = (x1 >> 3) & 0x11111111u;
+  e0 = (e0 | (e0 >> 3)) & 0x03030303u;
+  e1 = (e1 | (e1 >> 3)) & 0x03030303u;
+  e0 = (e0 | (e0 >> 6)) & 0x000F000Fu;
+  e1 = (e1 | (e1 >> 6)) & 0x000F000Fu;
+  e0 = (e0 | (e0 >> 12)) & 0xFFu;
+  e1 = (e1 | (e1 >> 12)) & 0xFFu;
+  return e0 | (e1 << 8);
 }
+
+// Staged tile, per wave: the 2-bit codes of its positions (16 per word) and
+// their invalid bits (not ACGTacgt; 16 per half-word), each behind a guard
+// of 64 positions ('-' chunks read from up to 45 positions before their
+// first codon; what they read there is masked off by the stream end).
+constexpr int kCodeGuard = 4;   // words of codes before position 0
+constexpr int kInvGuard = 4;    // half-words of invalid bits before position 0
 
 // One 16-residue chunk per lane.  kMode 0: every lane '+', 1: every lane
 // '-' (wave-uniform: table offsets fold into the LDS immediates), 2: mixed.
+// The chunk's 48 positions of 2-bit codes come from four staged words,
+// aligned by one funnel shift per word; codon k's index is then bits
+// [6k, 6k+6) of that 96-bit window (a bit-field extract), and its residue one
+// LDS byte read.  Consecutive chunks of a segment start 48 positions (3
+// words) apart, so the four word reads of a half-wave over one segment hit 32
+// different banks.  A tile holding a non-ACGT base (tile_inv) patches the
+// codons with an invalid base to 'X' from the staged invalid bits.
 template <int kMode>
-__device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* stage,
+__device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint32_t* codes,
+                                           const uint32_t* inv32, bool tile_inv,
                                            const uint8_t* tbl, const OrfSeg* seg,
                                            const uint32_t* bm, const uint32_t* pre, uint32_t q,
                                            uint32_t n_chunks) {
@@ -244,45 +257,60 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint8_t* sta
   __asm__("" : "+v"(m48));                   // from folding into a -48 v_mul_lo)
   const int32_t p = minus ? g.p0 - m48 : g.p0 + m48;
   // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed below)
-  const uint8_t* const src = stage + (minus ? p - 45 : p);
+  const int32_t P = minus ? p - 45 : p;
+  const uint32_t* const cw = codes + (P >> 4);
+  const uint32_t sh = 2u * (uint32_t)(P & 15);
+  const uint32_t X0 = cw[0], X1 = cw[1], X2 = cw[2], X3 = cw[3];
+  uint32_t Y[3];
+  Y[0] = __builtin_amdgcn_alignbit(X1, X0, sh);
+  Y[1] = __builtin_amdgcn_alignbit(X2, X1, sh);
+  Y[2] = __builtin_amdgcn_alignbit(X3, X2, sh);
   const uint8_t* const tb = kMode == 2 ? tbl + (minus ? 128 : 0) : tbl + (kMode == 1 ? 128 : 0);
-  // Consecutive chunks of a segment sit 48 bytes (12 banks) apart, so lanes
-  // q, q+8, q+16, q+24 of a half-wave would hit one bank with every staged
-  // byte read.  Lane group j = (q >> 3) & 3 reads its residue quads in the
-  // rotated order j, j+1, .. (3 banks further per step), which makes the 32
-  // reads of a half-wave over one segment conflict-free; the quads are
-  // rotated back in registers.
-  const uint32_t rj = (q >> 3) & 3u;
-  // byte offsets of the quads in read order, one per byte: 12 * ((s + rj) & 3)
-  const uint32_t qo = __builtin_amdgcn_alignbit(0x24180C00u, 0x24180C00u, 8u * rj);
-  uint32_t r[4];
-  // every codon index in flight before the first table read
-  uint32_t c[4][4];
+  uint32_t c[16];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const uint8_t* const qs = src + ((qo >> (8 * s)) & 0xFFu);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) c[s][i] = qs[3 * i];
+  for (int k = 0; k < 16; ++k) {
+    const int ob = 6 * k;
+    c[k] = ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
+                            : __builtin_amdgcn_alignbit(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
+           63u;
   }
+  uint32_t o[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    // three ops per quad: two byte pairs, then one perm; a quad of an
-    // all-'-' iteration is packed in reverse byte order (the reversal below
-    // is then a register renaming)
+  for (int s4 = 0; s4 < 4; ++s4) {
+    // a quad of an all-'-' iteration is packed in reverse byte order (the
+    // reversal below is then a register renaming)
     constexpr int k0 = kMode == 1 ? 3 : 0, k1 = kMode == 1 ? 2 : 1;
-    const uint32_t lo = (uint32_t)tb[c[s][k0]] | ((uint32_t)tb[c[s][k1]] << 8);
-    const uint32_t hi = (uint32_t)tb[c[s][3 - k1]] | ((uint32_t)tb[c[s][3 - k0]] << 8);
-    r[s] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+    const uint32_t lo = (uint32_t)tb[c[4 * s4 + k0]] | ((uint32_t)tb[c[4 * s4 + k1]] << 8);
+    const uint32_t hi = (uint32_t)tb[c[4 * s4 + 3 - k1]] | ((uint32_t)tb[c[4 * s4 + 3 - k0]] << 8);
+    o[s4] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
   }
-  uint32_t o[4];  // o[d] = r[(d - rj) & 3]: rotate by 2, then by 1
-  {
-    const bool j2 = (q & 16u) != 0, j1 = (q & 8u) != 0;
-    const uint32_t t0 = j2 ? r[2] : r[0], t1 = j2 ? r[3] : r[1];
-    const uint32_t t2 = j2 ? r[0] : r[2], t3 = j2 ? r[1] : r[3];
-    o[0] = j1 ? t3 : t0;
-    o[1] = j1 ? t0 : t1;
-    o[2] = j1 ? t1 : t2;
-    o[3] = j1 ? t2 : t3;
+  if (tile_inv) {
+    // codon k holds a non-ACGT base: any of invalid bits 3k .. 3k+2
+    const uint32_t* const iw = inv32 + (P >> 5);
+    const uint32_t s1 = (uint32_t)(P & 31);
+    const uint32_t I0 = iw[0], I1 = iw[1], I2 = iw[2];
+    const uint32_t Z0 = __builtin_amdgcn_alignbit(I1, I0, s1);
+    const uint32_t Z1 = __builtin_amdgcn_alignbit(I2, I1, s1);
+    const uint32_t A = Z0 | __builtin_amdgcn_alignbit(Z1, Z0, 1) | __builtin_amdgcn_alignbit(Z1, Z0, 2);
+    const uint32_t B = Z1 | (Z1 >> 1) | (Z1 >> 2);
+    const uint32_t bad0 = A & 0x49249249u;  // codons 0..10 (bits 3k)
+    const uint32_t bad1 = B & 0x00002492u;  // codons 11..15 (bits 3k - 32)
+    if (bad0 | bad1) {
+      const uint32_t f[4] = {bad0 & 0xFFFu, (bad0 >> 12) & 0xFFFu,
+                             ((bad0 >> 24) | (bad1 << 8)) & 0xFFFu, (bad1 >> 4) & 0xFFFu};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        // bits 0,3,6,9 -> bytes 0..3 of word j (ascending codons); byte-
+        // reversed where this iteration packed the '-' quads reversed
+        const uint32_t m = ((f[j] * 0x8421u) & 0x01010101u) * 0xFFu;
+        if constexpr (kMode == 1) {
+          const uint32_t mr = __builtin_amdgcn_perm(0u, m, 0x00010203u);
+          o[j] = (o[j] & ~mr) | (0x58585858u & mr);
+        } else {
+          o[j] = (o[j] & ~m) | (0x58585858u & m);
+        }
+      }
+    }
   }
   if constexpr (kMode == 1) {  // bytes already reversed: reverse the words
     uint32_t t = o[0];
@@ -320,7 +348,12 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   // the table's fixed address folds into the LDS immediates.
   __shared__ uint32_t s_tblw[64];
   __shared__ uint8_t s_code[256];  // byte -> 2-bit code, or 0x40 when not ACGTacgt
-  __shared__ uint4 s_stage[kOpsThreads / 64][kOrfVecs];
+  // staged codes (the histogram counters and the vector -> interval map
+  // first) and invalid bits, behind their guards (orf_chunks)
+  __shared__ __attribute__((aligned(16))) uint32_t
+      s_codes[kOpsThreads / 64][kCodeGuard + kOrfVecs + 8];
+  __shared__ __attribute__((aligned(16))) uint16_t
+      s_inv[kOpsThreads / 64][kInvGuard + kOrfVecs + 8];
   // per wave: the staging window's interval rows, then (same bytes) the
   // segment table and the chunk bitmap with its prefix counts
   constexpr int kScratch = 2 * (kOrf6RowCap + 1);
@@ -367,8 +400,12 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   const uint64_t nb_first = a.noff[rr0], ne_first = a.noff[rr0 + 1];
   uint64_t nb = 0, L = 0;
   bool rec = false;
+  uint32_t* const codes = s_codes[wave] + kCodeGuard;
+  uint16_t* const inv16 = s_inv[wave] + kInvGuard;
+  bool any_inv = false;  // this lane staged a non-ACGT base
   if (!kGenome) {
-    // raw bytes: all loads in flight at once, to LDS when they land
+    // raw bytes: all loads in flight at once, then 2-bit codes and invalid
+    // bits per 16-byte vector
     uint4 v[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
@@ -376,14 +413,26 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
       v[k] = *reinterpret_cast<const uint4*>(a.nuc + W0 + 16 * (uint64_t)t);
     }
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) s_stage[wave][lane + 64 * k] = v[k];
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+      uint32_t cd = 0, bad = 0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint32_t e = s_code[(w[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+        cd |= (e & 3u) << (2 * j);
+        bad |= (e >> 6) << j;
+      }
+      codes[lane + 64 * k] = cd;
+      inv16[lane + 64 * k] = (uint16_t)bad;
+      any_inv |= bad != 0;
+    }
   } else {
     // the window's intervals (<= kOrf6RowCap, host-planned), rebased once to
     // the window so that the per-vector math is 32-bit: {byte offset of the
     // plane word holding window position 0 (mod 2^32: only positions inside
     // the interval are read), 4 * nibble shift, window-relative start}
     uint4* const row = reinterpret_cast<uint4*>(s_scratch[wave]);
-    uint32_t* const cnt = reinterpret_cast<uint32_t*>(s_stage[wave]);  // 256 counters, then map
+    uint32_t* const cnt = codes;  // 256 counters, then the vector -> interval map
     const uint64_t e0 = a.tile_e0[tile];
     const int32_t wlen = (int32_t)(WE - W0);
     int32_t rel[2];
@@ -410,7 +459,7 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
                              (uint32_t)(A & 31u) | ((rw[h].y & kOrf6ExcRow) ? 32u : 0u),
                              (uint32_t)rel[h], (uint32_t)(A >> 5) << 2);
     }
-    s_stage[wave][lane] = make_uint4(0u, 0u, 0u, 0u);
+    reinterpret_cast<uint4*>(cnt)[lane] = make_uint4(0u, 0u, 0u, 0u);
     const uint32_t m = (uint32_t)(__popcll(__ballot(in[0])) + __popcll(__ballot(in[1])));
     __builtin_amdgcn_wave_barrier();
     // first interval of every vector: count interval starts per vector
@@ -424,11 +473,11 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     }
     __builtin_amdgcn_wave_barrier();
     {
-      const uint4 c = s_stage[wave][lane];  // vectors 4 lane .. 4 lane + 3
+      const uint4 c = reinterpret_cast<const uint4*>(cnt)[lane];  // vectors 4 lane .. + 3
       const uint32_t c0 = c.x, c1 = c0 + c.y, c2 = c1 + c.z, c3 = c2 + c.w;
       const uint32_t x = wave_scan(c3);
       const uint32_t base = x - c3 - 1;
-      s_stage[wave][lane] = make_uint4(base + c0, base + c1, base + c2, base + c3);
+      reinterpret_cast<uint4*>(cnt)[lane] = make_uint4(base + c0, base + c1, base + c2, base + c3);
     }
     __builtin_amdgcn_wave_barrier();
     // Codon indices straight from the 2-bit code plane: translation ignores
@@ -449,7 +498,7 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     uint32_t iv[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) iv[k] = min(cnt[lane + 64 * k], m - 1);
-    uint32_t wa[kPer][3], wb[kPer][3], xa[kPer][2], xb[kPer][2];
+    uint32_t wa[kPer][2], wb[kPer][2], xa[kPer][2], xb[kPer][2];
     // Windows without a flagged interval (most) skip the exception plane:
     // no loads, no address math, no merge (wave-uniform).
     // (the 64-bit ballot is tested before readfirstlane, which takes 32 bits:
@@ -465,12 +514,12 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
         const uint32_t t = lane + 64 * k;
         const int32_t t16 = 16 * (int32_t)t;
         const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];
-        const bool cross = (int32_t)r1.z < min(t16 + 18, wlen);
-        const auto va = __builtin_amdgcn_raw_buffer_load_b96(plane2, r0.x + 4u * t, 0, 0);
+        const bool cross = (int32_t)r1.z < min(t16 + 16, wlen);
+        const auto va = __builtin_amdgcn_raw_buffer_load_b64(plane2, r0.x + 4u * t, 0, 0);
         const auto vb =
-            __builtin_amdgcn_raw_buffer_load_b96(plane2, cross ? r1.x + 4u * t : 0xFFFFFFF0u, 0, 0);
+            __builtin_amdgcn_raw_buffer_load_b64(plane2, cross ? r1.x + 4u * t : 0xFFFFFFF0u, 0, 0);
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
+        for (int d = 0; d < 2; ++d) {
           wa[k][d] = va[d];
           wb[k][d] = vb[d];
         }
@@ -494,24 +543,22 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     else issue(std::false_type{});
     __builtin_amdgcn_sched_barrier(0);  // every window load is issued before the first is consumed
     uint32_t exact = 0;  // bit k: vector k takes the exact path below
-    bool any_exc = false;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const uint32_t t = lane + 64 * k;
       const int32_t t16 = 16 * (int32_t)t;
-      const int32_t et = min(t16 + 18, wlen);
+      const int32_t et = min(t16 + 16, wlen);
       const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];  // re-read: fewer live registers
       const bool cross = (int32_t)r1.z < et;
-      // positions [j0, 18) come from the second interval (none: j0 = 32)
+      // positions [j0, 16) come from the second interval (none: j0 = 32)
       const uint32_t j0 = cross ? (uint32_t)((int32_t)r1.z - t16) : 32u;
-      const uint64_t mb = j0 >= 32 ? 0ull : ~0ull << (2 * j0);
+      const uint32_t mb = j0 >= 16 ? 0u : ~0u << (2 * j0);
       const uint32_t sa = 2u * (r0.y & 15u), sb = 2u * (r1.y & 15u);
-      const uint32_t x0 = funnel4(wa[k][1], wa[k][0], sa), x1 = funnel4(wa[k][2], wa[k][1], sa);
-      const uint32_t b0 = funnel4(wb[k][1], wb[k][0], sb), b1 = funnel4(wb[k][2], wb[k][1], sb);
-      const uint32_t y0 = (b0 & (uint32_t)mb) | (x0 & ~(uint32_t)mb);
-      const uint32_t y1 = (b1 & (uint32_t)(mb >> 32)) | (x1 & ~(uint32_t)(mb >> 32));
+      const uint32_t x0 = funnel4(wa[k][1], wa[k][0], sa);
+      const uint32_t b0 = funnel4(wb[k][1], wb[k][0], sb);
+      const uint32_t y0 = (b0 & mb) | (x0 & ~mb);  // codes of positions 0..15
       if (cross && (int32_t)row[iv[k] + 2].z < et) exact |= 1u << k;
-      // exception bits of positions 0..17: bit j set = base j not ACGTacgt
+      // exception bits of positions 0..15: bit j set = base j not ACGTacgt
       uint32_t ex = 0;
       if (wexc) {
         const uint32_t ma = j0 >= 32 ? 0u : ~0u << j0;
@@ -519,48 +566,13 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
         const uint32_t vb = funnel4(xb[k][1], xb[k][0], ((r1.y & 31u) + 16u * t) & 31u);
         ex = (vb & ma) | (va & ~ma);
       }
-      any_exc |= ex != 0;
-      xa[k][0] = ex;  // reused below
-      // cidx byte i = codes of positions i, i+1, i+2 = bits [2i, 2i+6)
-      uint32_t o[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t z = j == 0 ? y0 : funnel4(y1, y0, 8u * j);
-        // byte k = bits [2k, 2k+6) of z: two full-rate 24-bit multiplies make
-        // non-overlapping copies of the low 12 bits (shifts 0 and 12 for
-        // bytes 0 and 2, 6 and 18 for bytes 1 and 3), then two masks
-        const uint32_t z12 = z & 0xFFFu;
-        uint32_t ev = __umul24(z12, 0x1001u), od = __umul24(z12, 0x40040u);
-        __asm__("" : "+v"(ev), "+v"(od));  // kept as v_mul_u32_u24
-        o[j] = (ev & 0x003F003Fu) | (od & 0x3F003F00u);
-      }
-      s_stage[wave][t] = make_uint4(o[0], o[1], o[2], o[3]);
-    }
-    if (__builtin_amdgcn_readfirstlane(__ballot(any_exc) != 0)) {
-      // codon i is invalid ('X') when any of positions i, i+1, i+2 is an
-      // exception: set bit 6 of its index
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) {
-        const uint32_t ex = xa[k][0];
-        if (ex) {
-          const uint32_t t = lane + 64 * k;
-          const uint32_t inv = ex | (ex >> 1) | (ex >> 2);
-          uint4 c = s_stage[wave][t];
-          uint32_t* const cw = reinterpret_cast<uint32_t*>(&c);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            uint32_t sp = __umul24((inv >> (4 * j)) & 15u, 0x204081u);  // bit k -> bit 8k
-            __asm__("" : "+v"(sp));  // not folded with the shift into a quarter-rate v_mul_lo
-            cw[j] |= (sp & 0x01010101u) << 6;
-          }
-          s_stage[wave][t] = c;
-        }
-      }
+      codes[t] = y0;
+      inv16[t] = (uint16_t)ex;
+      any_inv |= (ex & 0xFFFFu) != 0;
     }
     if (__builtin_amdgcn_readfirstlane(__ballot(exact != 0) != 0)) {
-      // Exact path (rare): vectors over an exception run or over three or
-      // more intervals rebuild their 18 positions from the nibble plane,
-      // interval by interval, as e-bytes (code | exception << 6).
+      // Exact path (rare): vectors over three or more intervals rebuild their
+      // 16 positions from the nibble plane, interval by interval.
       const __amdgpu_buffer_rsrc_t plane = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<uint32_t*>(a.nib), (short)0,
           (int)(uint32_t)min(a.nib_words * 4, (uint64_t)0xFFFFFFFFu), 0x00020000);
@@ -569,8 +581,8 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
         if (!((exact >> k) & 1u)) continue;
         const uint32_t t = lane + 64 * k;
         const int32_t t16 = 16 * (int32_t)t;
-        const int32_t et = min(t16 + 18, wlen);
-        uint32_t x[3] = {0u, 0u, 0u};  // nibbles of positions 0..17 (x[2]: 16, 17)
+        const int32_t et = min(t16 + 16, wlen);
+        uint32_t x[2] = {0u, 0u};  // nibbles of positions 0..15
         uint32_t i = iv[k];
         int32_t pos = t16;
         while (pos < et) {
@@ -579,12 +591,11 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
           // nibble-plane byte offset of the word holding window position 0
           const uint32_t nboff = 2u * r.x + 4u * ((r.y >> 3) & 1u);
           const uint32_t sh = 4u * (r.y & 7u);
-          const auto w = __builtin_amdgcn_raw_buffer_load_b128(plane, nboff + 8u * t, 0, 0);
-          const uint32_t c[3] = {funnel4(w[1], w[0], sh), funnel4(w[2], w[1], sh),
-                                 funnel4(w[3], w[2], sh)};
+          const auto w = __builtin_amdgcn_raw_buffer_load_b96(plane, nboff + 8u * t, 0, 0);
+          const uint32_t c[2] = {funnel4(w[1], w[0], sh), funnel4(w[2], w[1], sh)};
           const int32_t j = pos - t16, n = nxt - pos;
 #pragma unroll
-          for (int q = 0; q < 3; ++q) {
+          for (int q = 0; q < 2; ++q) {
             const int32_t lo = max(j - 8 * q, 0), hi = min(j + n - 8 * q, 8);
             if (lo < hi) {
               const uint32_t mh = hi >= 8 ? ~0u : (1u << (4 * hi)) - 1u;
@@ -596,27 +607,35 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
           pos = nxt;
           ++i;
         }
-        uint32_t e[6];
-        nibbles_to_e(x[0], e[0], e[1]);
-        nibbles_to_e(x[1], e[2], e[3]);
-        nibbles_to_e(x[2], e[4], e[5]);
-        s_stage[wave][t] = codon_indices(e);
+        codes[t] = nib_codes(x[0], x[1]);
+        const uint32_t bad = nib_exc16(x[0], x[1]);
+        inv16[t] = (uint16_t)bad;
+        any_inv |= bad != 0;
       }
     }
   }
-  const uint8_t* const stage = reinterpret_cast<const uint8_t*>(s_stage[wave]);
+  // guards and tail: defined words around the staged positions
+  if (lane < kCodeGuard) s_codes[wave][lane] = 0u;
+  if (lane < kInvGuard) s_inv[wave][lane] = 0u;
+  if (lane < 8) {
+    codes[kOrfVecs + lane] = 0u;
+    inv16[kOrfVecs + lane] = 0u;
+  }
+  const bool tile_inv = __builtin_amdgcn_readfirstlane(__ballot(any_inv) != 0);
+  const uint32_t* const inv32 = reinterpret_cast<const uint32_t*>(s_inv[wave] + kInvGuard);
+
   OrfSeg* const seg = reinterpret_cast<OrfSeg*>(s_scratch[wave]);
   uint32_t* const bm = reinterpret_cast<uint32_t*>(s_scratch[wave] + 2 * kOrfSegs);
   uint32_t* const pre = bm + kOrfRankWords;
-  bool staged = kGenome;  // the gather stages codon indices directly
+  bool first_batch = !kGenome;
   for (;; rb += kOrfBatch) {
     // ---- the batch's segments: one (record, stream) per lane
     const uint64_t r = rb + my_rec;
     rec = lane < kOrfSegs && r < a.n_rec;
-    if (staged) {
+    if (!first_batch) {
       nb = rec ? a.noff[r] : 0;
       L = rec ? a.noff[r + 1] - nb : 0;
-    } else {
+    } else {  // raw bytes: the offsets loaded with the staging loads
       nb = rec ? nb_first : 0;
       L = rec ? ne_first - nb_first : 0;
     }
@@ -649,36 +668,6 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
                       rb + kOrfBatch < a.n_rec;
     bm[lane] = 0u;
     bm[lane + 64] = 0u;
-    if (!staged) {  // cidx[p] = c[p] | c[p+1] << 2 | c[p+2] << 4 | invalid << 6
-      // in place, vector t after vector t+1's first bytes were read (LDS
-      // operations of a wave complete in order)
-#pragma unroll 1
-      for (int k = 0; k < kPer; ++k) {
-        const uint32_t t = lane + 64 * k;
-        const uint4 raw = s_stage[wave][t];
-        const uint32_t nxt =
-            reinterpret_cast<const uint32_t*>(s_stage[wave])[4 * min(t + 1, (uint32_t)kOrfVecs - 1)];
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t w[5] = {raw.x, raw.y, raw.z, raw.w, nxt};
-        uint32_t e[5];
-        if (kGenome) {
-#pragma unroll
-          for (int j = 0; j < 5; ++j) e[j] = w[j];
-        } else {
-#pragma unroll
-          for (int j = 0; j < 5; ++j) {
-            const uint32_t x = w[j];
-            e[j] = (uint32_t)s_code[x & 0xFFu] | ((uint32_t)s_code[(x >> 8) & 0xFFu] << 8);
-            if (j < 4)
-              e[j] |= ((uint32_t)s_code[(x >> 16) & 0xFFu] << 16) |
-                      ((uint32_t)s_code[x >> 24] << 24);
-          }
-        }
-        s_stage[wave][t] = codon_indices(e);
-        __builtin_amdgcn_wave_barrier();
-      }
-      staged = true;
-    }
     __builtin_amdgcn_wave_barrier();
     if (cnt) {
       const uint32_t start = incl - cnt;
@@ -703,11 +692,15 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     // ---- the batch's chunks, 64 at a time
     for (uint32_t q0 = 0; q0 < n_chunks; q0 += 64) {
       const uint32_t q = q0 + lane;
-      if (q0 + 64 <= n_minus) orf_chunks<1>(a, stage, s_tbl, seg, bm, pre, q, n_chunks);
-      else if (q0 >= n_minus) orf_chunks<0>(a, stage, s_tbl, seg, bm, pre, q, n_chunks);
-      else orf_chunks<2>(a, stage, s_tbl, seg, bm, pre, q, n_chunks);
+      if (q0 + 64 <= n_minus)
+        orf_chunks<1>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+      else if (q0 >= n_minus)
+        orf_chunks<0>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+      else
+        orf_chunks<2>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
     }
     if (!more) break;
+    first_batch = false;
     __builtin_amdgcn_wave_barrier();  // segment tables are rewritten
   }
 }
