@@ -229,89 +229,102 @@ __device__ __forceinline__ uint32_t nib_exc16(uint32_t x0, uint32_t x1) {
 constexpr int kCodeGuard = 4;   // words of codes before position 0
 constexpr int kInvGuard = 4;    // half-words of invalid bits before position 0
 
-// One 16-residue chunk per lane.  kMode 0: every lane '+', 1: every lane
+// 16-residue chunks, one per lane.  kMode 0: every lane '+', 1: every lane
 // '-' (wave-uniform: table offsets fold into the LDS immediates), 2: mixed.
-// The chunk's 48 positions of 2-bit codes come from four staged words,
-// aligned by one funnel shift per word; codon k's index is then bits
-// [6k, 6k+6) of that 96-bit window (a bit-field extract), and its residue one
-// LDS byte read.  Consecutive chunks of a segment start 48 positions (3
-// words) apart, so the four word reads of a half-wave over one segment hit 32
-// different banks.  A tile holding a non-ACGT base (tile_inv) patches the
-// codons with an invalid base to 'X' from the staged invalid bits.
+// A chunk's 48 positions of 2-bit codes come from four staged words, aligned
+// by one funnel shift per word; codon k's index is then bits [6k, 6k+6) of
+// that 96-bit window (a bit-field extract) and its residue one LDS byte read.
+// Consecutive chunks of a segment start 48 positions (3 words) apart, so the
+// word reads of a half-wave over one segment hit 32 different banks, and each
+// 128-entry residue table is one word per bank.  A tile holding a non-ACGT
+// base (tile_inv) patches codons with an invalid base to 'X' from the staged
+// invalid bits.  Each lane handles chunk q and, when the batch has them, chunk
+// q + 64 in the same pass: the two chains of dependent LDS reads (rank ->
+// segment -> codes -> residues) overlap.
+struct OrfChunk {
+  uint32_t Y[3];     // codes of positions P .. P+47
+  int32_t P;         // window position of codon 0 (ascending)
+  int32_t rem;       // residues left in the stream from this chunk
+  uint64_t dst;      // output byte offset
+  bool minus;
+};
+
 template <int kMode>
-__device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint32_t* codes,
-                                           const uint32_t* inv32, bool tile_inv,
-                                           const uint8_t* tbl, const OrfSeg* seg,
-                                           const uint32_t* bm, const uint32_t* pre, uint32_t q,
-                                           uint32_t n_chunks) {
-  if (q >= n_chunks) return;
-  // opaque per iteration: keeps the compiler from hoisting lane-invariant
-  // address terms of all three variants out of the chunk loop (and spilling)
+__device__ __forceinline__ OrfChunk orf_fetch(const uint32_t* codes, const OrfSeg* seg,
+                                              const uint32_t* bm, const uint32_t* pre,
+                                              uint32_t q) {
+  // opaque per call: keeps the compiler from hoisting lane-invariant address
+  // terms of all three variants out of the chunk loop (and spilling)
   __asm__ volatile("" : "+v"(q));
   const uint32_t wq = q >> 5;
   const uint32_t rank = pre[wq] + __popc(bm[wq] & (0xFFFFFFFFu >> (31 - (q & 31))));
   const OrfSeg g = seg[rank - 1];
-  const bool minus = kMode == 1 ? true : kMode == 0 ? false : g.rem0 < 0;
-  const int32_t rem = (minus ? -g.rem0 : g.rem0) - 16 * (int32_t)q;
+  OrfChunk h;
+  h.minus = kMode == 1 ? true : kMode == 0 ? false : g.rem0 < 0;
+  h.rem = (h.minus ? -g.rem0 : g.rem0) - 16 * (int32_t)q;
   int32_t m48 = (int32_t)__umul24(q, 48u);  // full-rate 24-bit multiply (kept
   __asm__("" : "+v"(m48));                   // from folding into a -48 v_mul_lo)
-  const int32_t p = minus ? g.p0 - m48 : g.p0 + m48;
-  // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed below)
-  const int32_t P = minus ? p - 45 : p;
-  const uint32_t* const cw = codes + (P >> 4);
-  const uint32_t sh = 2u * (uint32_t)(P & 15);
+  const int32_t p = h.minus ? g.p0 - m48 : g.p0 + m48;
+  // ascending codon positions: '+' p, p+3, ..; '-' p-45, .., p (reversed later)
+  h.P = h.minus ? p - 45 : p;
+  h.dst = g.out0 + 16 * (uint64_t)q;
+  const uint32_t* const cw = codes + (h.P >> 4);
+  const uint32_t sh = 2u * (uint32_t)(h.P & 15);
   const uint32_t X0 = cw[0], X1 = cw[1], X2 = cw[2], X3 = cw[3];
-  uint32_t Y[3];
-  Y[0] = __builtin_amdgcn_alignbit(X1, X0, sh);
-  Y[1] = __builtin_amdgcn_alignbit(X2, X1, sh);
-  Y[2] = __builtin_amdgcn_alignbit(X3, X2, sh);
-  const uint8_t* const tb = kMode == 2 ? tbl + (minus ? 128 : 0) : tbl + (kMode == 1 ? 128 : 0);
+  h.Y[0] = __builtin_amdgcn_alignbit(X1, X0, sh);
+  h.Y[1] = __builtin_amdgcn_alignbit(X2, X1, sh);
+  h.Y[2] = __builtin_amdgcn_alignbit(X3, X2, sh);
+  return h;
+}
+
+// Residue bytes of a fetched chunk, ascending codons; an all-'-' iteration
+// packs each quad in reverse byte order (the reversal is then a renaming).
+template <int kMode>
+__device__ __forceinline__ void orf_residues(const OrfChunk& h, const uint8_t* tbl, uint32_t o[4]) {
+  const uint8_t* const tb = kMode == 2 ? tbl + (h.minus ? 128 : 0) : tbl + (kMode == 1 ? 128 : 0);
   uint32_t c[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int ob = 6 * k;
-    c[k] = ((ob & 31) <= 26 ? (Y[ob >> 5] >> (ob & 31))
-                            : __builtin_amdgcn_alignbit(Y[(ob >> 5) + 1], Y[ob >> 5], ob & 31)) &
+    c[k] = ((ob & 31) <= 26 ? (h.Y[ob >> 5] >> (ob & 31))
+                            : __builtin_amdgcn_alignbit(h.Y[(ob >> 5) + 1], h.Y[ob >> 5], ob & 31)) &
            63u;
   }
-  uint32_t o[4];
 #pragma unroll
   for (int s4 = 0; s4 < 4; ++s4) {
-    // a quad of an all-'-' iteration is packed in reverse byte order (the
-    // reversal below is then a register renaming)
     constexpr int k0 = kMode == 1 ? 3 : 0, k1 = kMode == 1 ? 2 : 1;
     const uint32_t lo = (uint32_t)tb[c[4 * s4 + k0]] | ((uint32_t)tb[c[4 * s4 + k1]] << 8);
     const uint32_t hi = (uint32_t)tb[c[4 * s4 + 3 - k1]] | ((uint32_t)tb[c[4 * s4 + 3 - k0]] << 8);
     o[s4] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
   }
-  if (tile_inv) {
-    // codon k holds a non-ACGT base: any of invalid bits 3k .. 3k+2
-    const uint32_t* const iw = inv32 + (P >> 5);
-    const uint32_t s1 = (uint32_t)(P & 31);
-    const uint32_t I0 = iw[0], I1 = iw[1], I2 = iw[2];
-    const uint32_t Z0 = __builtin_amdgcn_alignbit(I1, I0, s1);
-    const uint32_t Z1 = __builtin_amdgcn_alignbit(I2, I1, s1);
-    const uint32_t A = Z0 | __builtin_amdgcn_alignbit(Z1, Z0, 1) | __builtin_amdgcn_alignbit(Z1, Z0, 2);
-    const uint32_t B = Z1 | (Z1 >> 1) | (Z1 >> 2);
-    const uint32_t bad0 = A & 0x49249249u;  // codons 0..10 (bits 3k)
-    const uint32_t bad1 = B & 0x00002492u;  // codons 11..15 (bits 3k - 32)
-    if (bad0 | bad1) {
-      const uint32_t f[4] = {bad0 & 0xFFFu, (bad0 >> 12) & 0xFFFu,
-                             ((bad0 >> 24) | (bad1 << 8)) & 0xFFFu, (bad1 >> 4) & 0xFFFu};
+}
+
+// Codons with a non-ACGT base (any of invalid bits 3k .. 3k+2) become 'X'.
+template <int kMode>
+__device__ __forceinline__ void orf_patch(const OrfChunk& h, const uint32_t* inv32, uint32_t o[4]) {
+  const uint32_t* const iw = inv32 + (h.P >> 5);
+  const uint32_t s1 = (uint32_t)(h.P & 31);
+  const uint32_t I0 = iw[0], I1 = iw[1], I2 = iw[2];
+  const uint32_t Z0 = __builtin_amdgcn_alignbit(I1, I0, s1);
+  const uint32_t Z1 = __builtin_amdgcn_alignbit(I2, I1, s1);
+  const uint32_t A = Z0 | __builtin_amdgcn_alignbit(Z1, Z0, 1) | __builtin_amdgcn_alignbit(Z1, Z0, 2);
+  const uint32_t B = Z1 | (Z1 >> 1) | (Z1 >> 2);
+  const uint32_t bad0 = A & 0x49249249u;  // codons 0..10 (bits 3k)
+  const uint32_t bad1 = B & 0x00002492u;  // codons 11..15 (bits 3k - 32)
+  const uint32_t f[4] = {bad0 & 0xFFFu, (bad0 >> 12) & 0xFFFu,
+                         ((bad0 >> 24) | (bad1 << 8)) & 0xFFFu, (bad1 >> 4) & 0xFFFu};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        // bits 0,3,6,9 -> bytes 0..3 of word j (ascending codons); byte-
-        // reversed where this iteration packed the '-' quads reversed
-        const uint32_t m = ((f[j] * 0x8421u) & 0x01010101u) * 0xFFu;
-        if constexpr (kMode == 1) {
-          const uint32_t mr = __builtin_amdgcn_perm(0u, m, 0x00010203u);
-          o[j] = (o[j] & ~mr) | (0x58585858u & mr);
-        } else {
-          o[j] = (o[j] & ~m) | (0x58585858u & m);
-        }
-      }
-    }
+  for (int j = 0; j < 4; ++j) {
+    // bits 0,3,6,9 -> bytes 0..3 of word j; byte-reversed where the quads
+    // were packed reversed
+    uint32_t m = ((f[j] * 0x8421u) & 0x01010101u) * 0xFFu;
+    if constexpr (kMode == 1) m = __builtin_amdgcn_perm(0u, m, 0x00010203u);
+    o[j] = (o[j] & ~m) | (0x58585858u & m);
   }
+}
+
+template <int kMode>
+__device__ __forceinline__ void orf_store(const Orf6Args& a, const OrfChunk& h, uint32_t o[4]) {
   if constexpr (kMode == 1) {  // bytes already reversed: reverse the words
     uint32_t t = o[0];
     o[0] = o[3];
@@ -319,21 +332,59 @@ __device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint32_t* co
     t = o[1];
     o[1] = o[2];
     o[2] = t;
-  } else if (minus) {
-    const uint32_t t0 = o[0], t1 = o[1];
-    o[0] = __builtin_amdgcn_perm(0u, o[3], 0x00010203u);
-    o[1] = __builtin_amdgcn_perm(0u, o[2], 0x00010203u);
-    o[2] = __builtin_amdgcn_perm(0u, t1, 0x00010203u);
-    o[3] = __builtin_amdgcn_perm(0u, t0, 0x00010203u);
+  } else if (kMode == 2) {
+    const uint32_t r0 = __builtin_amdgcn_perm(0u, o[3], 0x00010203u);
+    const uint32_t r1 = __builtin_amdgcn_perm(0u, o[2], 0x00010203u);
+    const uint32_t r2 = __builtin_amdgcn_perm(0u, o[1], 0x00010203u);
+    const uint32_t r3 = __builtin_amdgcn_perm(0u, o[0], 0x00010203u);
+    o[0] = h.minus ? r0 : o[0];
+    o[1] = h.minus ? r1 : o[1];
+    o[2] = h.minus ? r2 : o[2];
+    o[3] = h.minus ? r3 : o[3];
   }
-  if (rem < 16) {  // stream end: the padding bytes are zero
+  // stream end: the padding bytes are zero
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t drop = (uint32_t)min(max(4 * j + 4 - rem, 0), 4);  // bytes of word j
-      o[j] &= (uint32_t)(0xFFFFFFFFull >> (8 * drop));
-    }
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t drop = (uint32_t)min(max(4 * j + 4 - h.rem, 0), 4);  // bytes of word j
+    o[j] &= (uint32_t)(0xFFFFFFFFull >> (8 * drop));
   }
-  *reinterpret_cast<uint4*>(a.out + g.out0 + 16 * (uint64_t)q) = make_uint4(o[0], o[1], o[2], o[3]);
+  *reinterpret_cast<uint4*>(a.out + h.dst) = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int kMode>
+__device__ __forceinline__ void orf_chunks(const Orf6Args& a, const uint32_t* codes,
+                                           const uint32_t* inv32, bool tile_inv,
+                                           const uint8_t* tbl, const OrfSeg* seg,
+                                           const uint32_t* bm, const uint32_t* pre, uint32_t q,
+                                           uint32_t n_chunks) {
+  if (q >= n_chunks) return;
+  const OrfChunk h = orf_fetch<kMode>(codes, seg, bm, pre, q);
+  uint32_t o[4];
+  orf_residues<kMode>(h, tbl, o);
+  if (tile_inv) orf_patch<kMode>(h, inv32, o);
+  orf_store<kMode>(a, h, o);
+}
+
+// Chunks q and q + 64 (< n_chunks: the caller checks q + 64 - lane); both
+// chains are issued before either is consumed.
+template <int kMode>
+__device__ __forceinline__ void orf_chunk_pair(const Orf6Args& a, const uint32_t* codes,
+                                               const uint32_t* inv32, bool tile_inv,
+                                               const uint8_t* tbl, const OrfSeg* seg,
+                                               const uint32_t* bm, const uint32_t* pre,
+                                               uint32_t q, uint32_t n_chunks) {
+  const bool second = q + 64 < n_chunks;
+  const OrfChunk h0 = orf_fetch<kMode>(codes, seg, bm, pre, q);
+  const OrfChunk h1 = orf_fetch<kMode>(codes, seg, bm, pre, second ? q + 64 : q);
+  uint32_t o0[4], o1[4];
+  orf_residues<kMode>(h0, tbl, o0);
+  orf_residues<kMode>(h1, tbl, o1);
+  if (tile_inv) {
+    orf_patch<kMode>(h0, inv32, o0);
+    orf_patch<kMode>(h1, inv32, o1);
+  }
+  orf_store<kMode>(a, h0, o0);
+  if (second) orf_store<kMode>(a, h1, o1);
 }
 
 // kGenome = false: the records are bytes in a.nuc (Sequence.get_orfs batch).
@@ -690,14 +741,25 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     }
     __builtin_amdgcn_wave_barrier();
     // ---- the batch's chunks, 64 at a time
-    for (uint32_t q0 = 0; q0 < n_chunks; q0 += 64) {
+    for (uint32_t q0 = 0; q0 < n_chunks;) {
       const uint32_t q = q0 + lane;
-      if (q0 + 64 <= n_minus)
-        orf_chunks<1>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
-      else if (q0 >= n_minus)
-        orf_chunks<0>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
-      else
-        orf_chunks<2>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+      if (q0 + 64 < n_chunks) {  // two chunks per lane: q and q + 64
+        if (q0 + 128 <= n_minus)
+          orf_chunk_pair<1>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+        else if (q0 >= n_minus)
+          orf_chunk_pair<0>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+        else
+          orf_chunk_pair<2>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+        q0 += 128;
+      } else {
+        if (q0 + 64 <= n_minus)
+          orf_chunks<1>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+        else if (q0 >= n_minus)
+          orf_chunks<0>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+        else
+          orf_chunks<2>(a, codes, inv32, tile_inv, s_tbl, seg, bm, pre, q, n_chunks);
+        q0 += 64;
+      }
     }
     if (!more) break;
     first_batch = false;
@@ -795,18 +857,20 @@ void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_s
   out->t0.push_back(total);
 }
 
+constexpr int kOrf6BlocksPerCu = 7;
+
 void launch_orf6(const Orf6Args& a, bool genome, hipStream_t s) {
   if (a.n_tiles == 0) return;
   const uint64_t blocks = (a.n_tiles + kOpsThreads / 64 - 1) / (kOpsThreads / 64);
   if (genome) {
-    // Occupancy knob for A/B (MAGOT_ORF6_BLOCKS_PER_CU; default no cap: 6
-    // blocks per CU, LDS-limited).  Unlike extract_kernel this kernel wants
-    // every wave it can get: caps of 5 / 4 blocks ran 6 % / 19 % slower, and a
-    // 7-block build (row cap 95, 32-word chunk bitmap) was no faster.
+    // Blocks per CU (MAGOT_ORF6_BLOCKS_PER_CU overrides; 0: no cap).  With
+    // codes staged (14.6 KB LDS, 52 VGPRs) 8 blocks fit; 7 measured best:
+    // 1.4825 / 1.4839 / 1.4799 ms per C5 step against 1.508 / 1.5071 / 1.5091
+    // uncapped and 1.4868 / 1.488 / 1.4898 at 6 (one box, alternating runs).
     static const size_t pad = [] {
       const char* env = getenv("MAGOT_ORF6_BLOCKS_PER_CU");
       return occupancy_lds_pad(reinterpret_cast<const void*>(orf6_kernel<true>), kOpsThreads,
-                               env ? atoi(env) : 0);
+                               env ? atoi(env) : kOrf6BlocksPerCu);
     }();
     hipLaunchKernelGGL(orf6_kernel<true>, dim3((uint32_t)blocks), dim3(kOpsThreads), pad, s, a);
   } else
