@@ -602,14 +602,16 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     }
     return MAGOT_OK;
   };
-  // the large tile, or the small one for plans too small to fill the chip
-  // several times over (MAGOT_EXTRACT_LANE_CHUNKS=3|5 forces one, for A/Bs)
+  // the large tile, or the small one for translating plans too small to fill
+  // the chip several times over (MAGOT_EXTRACT_LANE_CHUNKS=3|5 forces one, for
+  // A/Bs); nucleotide-only plans keep the large tile (C2: 0.0164 vs 0.0172 ms)
   uint32_t lane_chunks = kLaneChunksLarge;
   if (int rc = cut(tile_bytes(kLaneChunksLarge))) return rc;
   const char* lc_env = std::getenv("MAGOT_EXTRACT_LANE_CHUNKS");
   const int lc_force = lc_env ? std::atoi(lc_env) : 0;
   if (lc_force == kLaneChunksSmall ||
-      (lc_force != kLaneChunksLarge && tile_start.size() < kSmallTilePlan)) {
+      (lc_force != kLaneChunksLarge && (outputs & MAGOT_OUT_PEP) &&
+       tile_start.size() < kSmallTilePlan)) {
     lane_chunks = kLaneChunksSmall;
     if (int rc = cut(tile_bytes(kLaneChunksSmall))) return rc;
   }

@@ -82,9 +82,10 @@ constexpr int kThreads = 256;                 // one workgroup = 4 independent w
 constexpr int kWaves = kThreads / 64;
 constexpr int kChunk = 16;                    // bytes per lane-store
 // Chunk slots per lane per tile: 5 (5072-byte tiles) for large plans; 3
-// (3024-byte tiles) for plans too small to fill the chip several times over,
-// where the launch tail dominates (one GPU's share of an 8-GPU C4 job: -3.5 %
-// per launch, A/B in DESIGN.md; at full C3 size 4 slots are +3.6 % slower).
+// (3024-byte tiles) for translating plans too small to fill the chip several
+// times over (one GPU's share of an 8-GPU C4 job: -3.5 % per launch; 4-GPU
+// share -2.7 %; but the 2-GPU share +8 %, C2 (nucleotides only) +5.5 %, and at
+// full C3 size 4 slots are +3.6 % slower; A/Bs in DESIGN.md).
 constexpr int kLaneChunksLarge = 5, kLaneChunksSmall = 3;
 constexpr int kLaneChunks = kLaneChunksLarge;   // the larger tile (LDS sizing, clamps)
 constexpr int kSlots = 64 * kLaneChunks;        // 320 chunk slots per wave tile
