@@ -367,6 +367,17 @@ def test_c3_full_size_vs_c_oracle():
 
 
 @pytest.mark.slow
+def test_c3_full_size_small_tiles_vs_c_oracle(monkeypatch, tile_size):
+    """C3 at full size cut into the small 3-slot tiles (the size one GPU's
+    share of the multi-GPU job takes), byte for byte."""
+    if tile_size != 'auto':
+        pytest.skip('one run is enough')
+    monkeypatch.setenv('MAGOT_EXTRACT_LANE_CHUNKS', '3')
+    w = synth.make('C3')
+    check_against_oracle(w)
+
+
+@pytest.mark.slow
 def test_c5_full_size_six_frames_vs_c_oracle():
     """BASELINE configs[4] at its stated size (3 Gb genome, 2M transcripts):
     the fused gather + six-frame kernel, ALL six frames of ALL records against
