@@ -250,6 +250,17 @@ int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* s
                           const uint64_t* pep_off, uint8_t* out);
 
 /*
+ * Single-sequence forms of the two (the SURVEY 8(b) sketch), same semantics.
+ * magot_revcomp: out holds len bytes.  magot_translate: standard code, frame
+ * >= 0 (MAGOT_ERR_UNSUPPORTED below: the Python layer lays negative frames out
+ * itself), strand '+' or '-', trimX 0/1; out holds len/3 bytes; *out_len =
+ * residues written, or -1 where the reference returns None.
+ */
+int magot_revcomp(magot_ctx* ctx, const uint8_t* seq, uint64_t len, uint8_t* out);
+int magot_translate(magot_ctx* ctx, const uint8_t* seq, uint64_t len, int frame, int strand,
+                    int trimX, uint8_t* out, int64_t* out_len);
+
+/*
  * Sequence.translate with an arbitrary codon `library` (genome.py:795-818:
  * any dict -- keys that are not ACGT triplets, e.g. 'NNN', multi-character
  * values -- and any integer frame, negative included).  The caller lays out

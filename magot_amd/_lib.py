@@ -31,7 +31,7 @@ EXPORTS = (
     'magot_run', 'magot_plan_time', 'magot_plan_time_b2b', 'magot_plan_device_outputs',
     'magot_plan_algorithmic_bytes',
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
-    'magot_codon_symbols',
+    'magot_codon_symbols', 'magot_revcomp', 'magot_translate',
     'magot_gff_plan', 'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
     'magot_gffplan_selections', 'magot_cds_scan', 'magot_cds_render',
     'magot_genome_export', 'magot_genome_copy_arena', 'magot_genome_attach',
@@ -98,6 +98,9 @@ def _declare(lib):
                                                  _vp, _vp]),
         'magot_codon_symbols': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32,
                                                _vp, _vp]),
+        'magot_revcomp': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp]),
+        'magot_translate': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, _vp, _i64p]),
         'magot_gff_plan': (ctypes.c_int, [_vp, ctypes.c_uint64,
                                           ctypes.POINTER(ctypes.c_char_p), _u64p, ctypes.c_uint32,
                                           ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(_vp),

@@ -996,6 +996,51 @@ int magot_codon_symbols(magot_ctx* ctx, const uint8_t* seq, uint64_t n_codons,
   return MAGOT_OK;
 }
 
+// --- single sequences (SURVEY 8(b) sketch) ---------------------------------
+
+int magot_revcomp(magot_ctx* ctx, const uint8_t* seq, uint64_t len, uint8_t* out) {
+  const uint64_t off[2] = {0, len};
+  return magot_revcomp_batch(ctx, seq, off, 1, out);
+}
+
+int magot_translate(magot_ctx* ctx, const uint8_t* seq, uint64_t len, int frame, int strand,
+                    int trimX, uint8_t* out, int64_t* out_len) {
+  if (!out_len || (len && !seq)) {
+    set_error("magot_translate: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (strand != '+' && strand != '-') {
+    set_error("magot_translate: strand must be '+' or '-'");
+    return MAGOT_ERR_ARG;
+  }
+  if (frame < 0) {
+    set_error("magot_translate: negative frame (the Python layer lays those out itself)");
+    return MAGOT_ERR_UNSUPPORTED;
+  }
+  const uint64_t off[2] = {0, len};
+  const int32_t fr = frame;
+  uint64_t poff[2];
+  int64_t codons = 0;
+  if (int rc = magot_translate_sizes(off, 1, &fr, poff, &codons)) return rc;
+  if (codons < 0) {  // translate() returns None (len <= 2 + frame)
+    *out_len = -1;
+    return MAGOT_OK;
+  }
+  if (codons && !out) {
+    set_error("magot_translate: null output");
+    return MAGOT_ERR_ARG;
+  }
+  const uint8_t st = (uint8_t)strand;
+  if (int rc = magot_translate_batch(ctx, seq, off, 1, &fr, &st, nullptr, poff, out)) return rc;
+  int64_t n = codons;
+  if (trimX && n > 0 && out[0] == 'X') {  // genome.py:819-821
+    std::memmove(out, out + 1, (size_t)(n - 1));
+    --n;
+  }
+  *out_len = n;
+  return MAGOT_OK;
+}
+
 // --- six-frame translation (Sequence.get_orfs, genome.py:824-851) ----------
 
 int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,

@@ -77,6 +77,31 @@ def test_translate_kat_batch():
         assert g == w, (s, f, st, t)
 
 
+def test_single_sequence_abi_kat():
+    """magot_translate / magot_revcomp (single-sequence C entry points)
+    against the reference's KATs: frames 0-4, both strands, trimX on/off,
+    -1 where translate() returns None."""
+    import ctypes
+    from magot_amd import _lib
+    L = _lib.lib()
+    ctx = _lib.default_context()
+    for r in _json('kat.json'):
+        seq = r['seq'].encode('latin-1')
+        buf = (ctypes.c_uint8 * max(len(seq), 1)).from_buffer_copy(seq or b'\0')
+        out = (ctypes.c_uint8 * max(len(seq), 1))()
+        _lib.check(L.magot_revcomp(ctx.handle, buf, len(seq), out), 'magot_revcomp')
+        assert bytes(out)[:len(seq)].decode('latin-1') == r['revcomp']
+        for key, want in r['translate'].items():
+            if isinstance(want, dict):
+                continue
+            f, st, trim = int(key[0]), key[1], int(key[2])
+            n = ctypes.c_int64()
+            _lib.check(L.magot_translate(ctx.handle, buf, len(seq), f, ord(st), trim, out,
+                                         ctypes.byref(n)), 'magot_translate')
+            got = None if n.value < 0 else bytes(out)[:n.value].decode('latin-1')
+            assert got == want, (r['seq'], key)
+
+
 def test_sequence_api_kat():
     S = G.Sequence('ATGGCCTTTAAACCCGGGTAG')
     assert S.translate() == 'MAFKPG*'
