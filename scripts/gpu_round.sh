@@ -9,7 +9,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
-# stages: tests slow bench driver c2 c5 multi kt kt5 kt2 pmc
+# stages: tests slow bench driver c2 c5 multi rehearse kt kt5 kt2 pmc smoke
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
 has() { [[ " $STAGES " == *" $1 "* ]]; }
@@ -49,6 +49,13 @@ if has kt; then
   grep -h extract_kernel $OUT/kt/kt_kernel_stats.csv
   cat $OUT/kt.json
 fi
+if has rehearse; then
+  # one GPU's share of the K-GPU C4 job (bench.py --rehearse-shard K:r)
+  for kr in 2:0 4:0 8:0 8:7; do
+    timeout -k 10 300 python $BENCH --rehearse-shard $kr --steps 300 --no-cpu-baseline > $OUT/rehearse_${kr/:/_}.json 2> $OUT/rehearse.err || { tail -20 $OUT/rehearse.err; exit 1; }
+    python3 -c "import json;d=json.load(open('$OUT/rehearse_${kr/:/_}.json'));r=d['roofline'];print('$kr', round(d['ms_per_step'],5), round(r['kernel_ms'],5), round(r['frac'],4), d['parity'][:20])"
+  done
+fi
 for cfg in C5 C2; do
   if has kt${cfg:1}; then
     rm -rf $OUT/kt_$cfg
@@ -69,4 +76,8 @@ if has pmc; then
     if [ $rc -ne 0 ]; then echo "pmc group $i failed rc=$rc"; tail -3 $OUT/pmc$i.log; [ $rc -ge 124 ] && exit 1; fi
   done
   python scripts/pmc_summary.py $OUT > $OUT/pmc_summary.json && cat $OUT/pmc_summary.json
+fi
+if has smoke; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
+  tail -1 $OUT/smoke.log
 fi
