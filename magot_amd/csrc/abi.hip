@@ -1190,8 +1190,68 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   rows[2 * ne] = 0;
   rows[2 * ne + 1] = total_nuc;
   starts[ne] = total_nuc;
+  // Processing order.  The kernel walks a concatenation of the records; the
+  // output keeps record order through the per-stream offsets, so the walk may
+  // follow the genome instead: records sorted by the plane position of their
+  // first interval put neighbouring loci into concurrently running tiles (one
+  // XCD sweeps one contiguous range), whose plane reads then share L2 lines.
+  // MAGOT_ORF6_ORDER=record keeps record order.
+  std::vector<uint64_t> noff_k, soff_k;
+  uint64_t ne_k = ne;
+  {
+    const char* env = getenv("MAGOT_ORF6_ORDER");
+    const bool genome_order = !(env && std::strcmp(env, "record") == 0);
+    const uint64_t n = o->n_rec;
+    const uint64_t* noff = p->nuc_off.data();
+    if (genome_order && ne && n > 1) {
+      std::vector<uint64_t> ie(n + 1), key(n), perm(n);
+      uint64_t i = 0;
+      for (uint64_t r = 0; r < n; ++r) {  // record r's intervals: [ie[r], ie[r+1])
+        while (i < ne && starts[i] < noff[r]) ++i;
+        ie[r] = i;
+      }
+      ie[n] = ne;
+      for (uint64_t r = 0; r < n; ++r)
+        key[r] = noff[r + 1] > noff[r] && ie[r] < ie[r + 1] ? rows[2 * ie[r]] + starts[ie[r]]
+                                                             : ~0ull;
+      for (uint64_t r = 0; r < n; ++r) perm[r] = r;
+      std::stable_sort(perm.begin(), perm.end(),
+                       [&](uint64_t x, uint64_t y) { return key[x] < key[y]; });
+      noff_k.resize(n + 1);
+      soff_k.resize(6 * n + 1);
+      std::vector<uint64_t> rows_k(2 * (ne + 1)), starts_k(ne + 1);
+      uint64_t j = 0;
+      noff_k[0] = 0;
+      for (uint64_t k = 0; k < n; ++k) {
+        const uint64_t r = perm[k];
+        noff_k[k + 1] = noff_k[k] + (noff[r + 1] - noff[r]);
+        for (int s = 0; s < 6; ++s) soff_k[6 * k + s] = o->host_soff[6 * r + s];
+        for (uint64_t e = ie[r]; e < ie[r + 1]; ++e) {
+          const uint64_t st = starts[e];
+          if (starts[e + 1] == st || st >= noff[r + 1]) continue;  // empty
+          const uint64_t st_k = noff_k[k] + (st - noff[r]);
+          rows_k[2 * j] = rows[2 * e] + st - st_k;  // the same unified anchor
+          rows_k[2 * j + 1] = st_k | (rows[2 * e + 1] & kOrf6ExcRow);
+          starts_k[j] = st_k;
+          ++j;
+        }
+      }
+      soff_k[6 * n] = o->host_soff[6 * n];
+      rows_k[2 * j] = 0;
+      rows_k[2 * j + 1] = total_nuc;
+      starts_k[j] = total_nuc;
+      rows_k.resize(2 * (j + 1));
+      starts_k.resize(j + 1);
+      rows.swap(rows_k);
+      starts.swap(starts_k);
+      ne_k = j;
+    } else {
+      noff_k.assign(noff, noff + n + 1);
+      soff_k = o->host_soff;
+    }
+  }
   Orf6Tiles tiles;
-  orf6_plan_tiles(p->nuc_off.data(), o->n_rec, starts.data(), ne, &tiles);
+  orf6_plan_tiles(noff_k.data(), o->n_rec, starts.data(), ne_k, &tiles);
   const uint64_t n_tiles = tiles.r0.size();
   uint8_t lut[64], tables[256];
   if (lut64) std::memcpy(lut, lut64, 64);
@@ -1201,7 +1261,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   const uint64_t o_off = cv.take<uint64_t>(o->n_rec + 1);
   const uint64_t o_soff = cv.take<uint64_t>(6 * o->n_rec + 1);
   const uint64_t o_out = cv.take<uint8_t>(o->total + 64);
-  const uint64_t o_rows = cv.take<uint64_t>(2 * (ne + 1));
+  const uint64_t o_rows = cv.take<uint64_t>(2 * (ne_k + 1));
   const uint64_t o_t0 = cv.take<uint64_t>(n_tiles + 1);
   const uint64_t o_r0 = cv.take<uint32_t>(n_tiles);
   const uint64_t o_e0 = cv.take<uint32_t>(n_tiles);
@@ -1222,8 +1282,8 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   launch_exc1(p->args.nib, nib_words, exc1, ctx->stream);
   MAGOT_HIP_TRY(hipGetLastError());
   MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
-  MAGOT_HIP_TRY(up(o_off, p->nuc_off.data(), (o->n_rec + 1) * 8));
-  MAGOT_HIP_TRY(up(o_soff, o->host_soff.data(), (6 * o->n_rec + 1) * 8));
+  MAGOT_HIP_TRY(up(o_off, noff_k.data(), (o->n_rec + 1) * 8));
+  MAGOT_HIP_TRY(up(o_soff, soff_k.data(), (6 * o->n_rec + 1) * 8));
   MAGOT_HIP_TRY(up(o_rows, rows.data(), rows.size() * 8));
   MAGOT_HIP_TRY(up(o_t0, tiles.t0.data(), (n_tiles + 1) * 8));
   MAGOT_HIP_TRY(up(o_r0, tiles.r0.data(), n_tiles * 4));
@@ -1238,7 +1298,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   a.exc1 = exc1;
   a.exc1_words = exc1_words;
   a.rows = reinterpret_cast<const uint64_t*>(base + o_rows);
-  a.n_rows = ne;
+  a.n_rows = ne_k;
   a.noff = reinterpret_cast<const uint64_t*>(base + o_off);
   a.n_rec = o->n_rec;
   a.total = total_nuc;
