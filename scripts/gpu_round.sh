@@ -12,6 +12,7 @@ STAGES=${*:-tests slow bench kt pmc}
 # stages: tests slow bench driver c2 c5 multi rehearse kt kt5 kt2 pmc smoke
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
+bash scripts/box_info.sh $OUT/box_before
 has() { [[ " $STAGES " == *" $1 "* ]]; }
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m "gpu and not slow" -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
@@ -81,3 +82,4 @@ if has smoke; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
   tail -1 $OUT/smoke.log
 fi
+bash scripts/box_info.sh $OUT/box_after
