@@ -9,7 +9,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
-# stages: tests slow bench driver c2 c5 multi rehearse kt kt5 kt2 pmc smoke
+# stages: tests slow bench driver c2 c5 multi rehearse kt kt5 kt2 pmc traffic smoke
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
 bash scripts/box_info.sh $OUT/box_before
@@ -77,6 +77,18 @@ if has pmc; then
     if [ $rc -ne 0 ]; then echo "pmc group $i failed rc=$rc"; tail -3 $OUT/pmc$i.log; [ $rc -ge 124 ] && exit 1; fi
   done
   python scripts/pmc_summary.py $OUT > $OUT/pmc_summary.json && cat $OUT/pmc_summary.json
+fi
+if has traffic; then
+  # HBM bytes per launch (FETCH_SIZE, WRITE_SIZE passes) of the C3, C5 and C2
+  # lines: scripts/pmc_json.py DIR CONFIG KERNEL turns each into profiles/pmc_<config>.json
+  for cfg in C3:extract_kernel C5:orf6_kernel C2:extract_kernel; do
+    c=${cfg%%:*}
+    for grp in FETCH_SIZE WRITE_SIZE; do
+      rm -rf $OUT/traffic_$c/$grp
+      timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/traffic_$c/$grp -o pmc -- python bench.py --config $c --steps 5 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline > $OUT/traffic_$c.$grp.log 2>&1 || { echo "traffic $c $grp failed"; tail -3 $OUT/traffic_$c.$grp.log; exit 1; }
+    done
+  done
+  echo traffic ok
 fi
 if has smoke; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -20 $OUT/smoke.log; exit 1; }
