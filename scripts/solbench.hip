@@ -1,0 +1,253 @@
+// Speed-of-light replays of the two measured kernels' memory traffic, with
+// no decode work: what the memory system gives a launch of the same shape
+// (waves, bytes written per wave and how, line fills per wave), so a kernel's
+// time can be read against what its own bytes allow and not only against the
+// 8 TB/s spec peak.
+//   hipcc -O3 --offload-arch=gfx950 scripts/solbench.hip -o /tmp/solbench
+//
+// c3: one wave per extraction tile (C3: 118,356 tiles of 5072 nucleotide
+//     bytes + their residues, 16-B-aligned and contiguous, non-temporal
+//     16-B stores as extract_kernel; L scattered 12-B window loads over the
+//     two 1-GB nibble planes, each one 128-B line fill; 6 blocks of 4 waves
+//     per CU as the launch cap).
+// c5: one wave per orf6 tile (605,096 tiles): R residue bytes per wave in
+//     runs of one record's six streams (~2.1 KB) at scattered 16-B-aligned
+//     places (the genome-order walk writes records in an order unrelated to
+//     their output offsets), plain 16-B stores, one store per lane per
+//     pass as orf6_kernel's chunk loop; L line fills per wave from a 1.5-GB
+//     code plane, walked in genome order (neighbouring tiles read
+//     neighbouring lines).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e = (x);                                                          \
+    if (e != hipSuccess) {                                                       \
+      printf("%s: %s\n", #x, hipGetErrorString(e));                              \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  return x ^ (x >> 33);
+}
+
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v, bool nt) {
+  v4u x = {v.x, v.y, v.z, v.w};
+  if (nt) __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
+  else *reinterpret_cast<v4u*>(p) = x;
+}
+
+struct C3Args {
+  const uint8_t* plane;
+  uint64_t plane_lines;
+  uint8_t* nuc;
+  uint8_t* pep;
+  uint32_t ntiles, lines, nuc_bytes, pep_bytes;
+  uint32_t* sink;
+  uint32_t win_tiles;     // reads: inside a moving window (one contig) of this many tiles (0: anywhere)
+  uint64_t win_lines;     // lines per window
+};
+
+__global__ __launch_bounds__(256) void c3_replay(C3Args a) {
+  const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= a.ntiles) return;
+  uint32_t acc = 0;
+  // scattered window loads, all in flight at once
+  uint3 v[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t l = lane + 64 * k;
+    const uint64_t line = a.win_tiles ? ((w / a.win_tiles) * a.win_lines + mix(w * 256 + l) % a.win_lines) % a.plane_lines
+                                      : mix(w * 256 + l) % a.plane_lines;
+    v[k] = l < a.lines ? *reinterpret_cast<const uint3*>(a.plane + line * 128 + 16 * (l & 7))
+                       : make_uint3(0, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z;
+  // nucleotide chunks, 5 slots per lane, then the residue chunks
+  uint8_t* const n0 = a.nuc + w * a.nuc_bytes;
+#pragma unroll
+  for (int s = 0; s < 5; ++s) {
+    const uint32_t c = 64 * s + lane;
+    if (16 * c < a.nuc_bytes) st16(n0 + 16 * c, make_uint4(acc, c, s, (uint32_t)w), true);
+  }
+  uint8_t* const p0 = a.pep + w * a.pep_bytes;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const uint32_t c = 64 * s + lane;
+    if (16 * c < a.pep_bytes) st16(p0 + 16 * c, make_uint4(acc, c, s, (uint32_t)w), true);
+  }
+  if (acc == 0x12345678u) *a.sink = acc;
+}
+
+struct C5Args {
+  const uint8_t* plane;
+  uint64_t plane_lines;
+  uint8_t* out;
+  uint64_t out_runs;  // run slots of run_bytes in the output
+  uint32_t ntiles, lines, run_bytes, runs;
+  uint32_t* sink;
+  uint32_t win_tiles;  // scattered runs: within the output window of this many tiles (0: anywhere)
+};
+
+// kSeq: runs laid out in walk order (tile w's runs follow tile w-1's), as
+// the record-order walk writes; else scattered (genome-order walk)
+template <bool kSeq, bool kNt>
+__global__ __launch_bounds__(256) void c5_replay(C5Args a) {
+  const uint32_t xnb = gridDim.x, xb = blockIdx.x;
+  const uint32_t xq = xnb >> 3, xr = xnb & 7, xcd = xb & 7, xk = xb >> 3;
+  const uint32_t vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  const uint64_t w = (uint64_t)vb * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= a.ntiles) return;
+  // genome-order reads: tile w's lines follow tile w-1's
+  uint32_t acc = 0;
+  {
+    const uint32_t l = lane;
+    const uint64_t line = (w * a.lines + l) % a.plane_lines;
+    const uint2 x = l < a.lines ? *reinterpret_cast<const uint2*>(a.plane + line * 128 + 8 * (l & 15))
+                                : make_uint2(0, 0);
+    acc = x.x ^ x.y;
+  }
+  // residue runs: the wave's records, one run of run_bytes each, at
+  // scattered places; 16-B chunks q = 64 i + lane over the concatenated runs
+  const uint32_t per = a.run_bytes / 16, total = per * a.runs;
+  for (uint32_t q = lane; q < total; q += 64) {
+    const uint32_t r = q / per, c = q - r * per;
+    const uint64_t wr = (uint64_t)a.win_tiles * a.runs;
+    const uint64_t slot = kSeq ? (w * a.runs + r) % a.out_runs
+                          : a.win_tiles ? ((w / a.win_tiles) * wr + mix(w * 64 + r) % wr) % a.out_runs
+                                        : mix(w * 64 + r) % a.out_runs;
+    st16(a.out + slot * a.run_bytes + 16 * c, make_uint4(acc, q, r, (uint32_t)w), kNt);
+  }
+  if (acc == 0x12345678u) *a.sink = acc;
+}
+
+// occupancy cap as the product launches use it: dynamic LDS nobody touches
+static size_t lds_pad(const void* fn, int want) {
+  int per = 0;
+  CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0));
+  if (want <= 0 || want >= per) return 0;
+  return 160 * 1024 / want - 1024;
+}
+
+int main(int argc, char** argv) {
+  const char* mode = argc > 1 ? argv[1] : "c3";
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  uint32_t* sink;
+  CK(hipMalloc(&sink, 4));
+  int ncu = 0;
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  auto timeit = [&](auto launch, const char* name, double wbytes, double rbytes) {
+    float ms = 0;
+    for (int i = 0; i < 50; ++i) launch();  // settle
+    CK(hipDeviceSynchronize());
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(hipEventRecord(e0));
+      for (int i = 0; i < 100; ++i) launch();
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ms /= 100;
+      printf("%-44s %.4f ms  writes %.3f GB  line fills %.3f GB  %.0f GB/s\n", name, ms,
+             wbytes / 1e9, rbytes / 1e9, (wbytes + rbytes) / (ms * 1e6));
+    }
+  };
+  if (!strcmp(mode, "c3")) {
+    // C3 (profiles/r03_close2): 118,356 tiles; 600.3 MB nucleotides and
+    // 199.9 MB residues; PMC line fills 0.86 GB per launch (~57 per tile)
+    const uint32_t ntiles = 118356, nuc = 5072, pep = 1696;
+    const uint64_t plane = 2ull << 30;
+    uint8_t *pl, *o1, *o2;
+    CK(hipMalloc(&pl, plane));
+    CK(hipMalloc(&o1, (uint64_t)ntiles * nuc));
+    CK(hipMalloc(&o2, (uint64_t)ntiles * pep));
+    CK(hipMemset(pl, 1, plane));
+    const size_t pad = lds_pad(reinterpret_cast<const void*>(c3_replay), 6);
+    const int grid = (int)((ntiles + 3) / 4);
+    for (uint32_t lines : {0u, 57u, 96u}) {
+      C3Args a{pl, plane / 128, o1, o2, ntiles, lines, nuc, pep, sink, 0u, 0u};
+      char nm[96];
+      snprintf(nm, sizeof nm, "c3 replay: %u line fills per tile", lines);
+      timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, a); }, nm,
+             (double)ntiles * (nuc + pep), (double)ntiles * lines * 128);
+    }
+    C3Args a{pl, plane / 128, o1, o2, ntiles, 57u, nuc, 0u, sink, 0u, 0u};
+    timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, a); },
+           "c3 replay: nucleotide stores only + 57 fills", (double)ntiles * nuc,
+           (double)ntiles * 57 * 128);
+    C3Args c{pl, plane / 128, o1, o2, ntiles, 57u, 0u, 0u, sink, 0u, 0u};
+    timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, c); },
+           "c3 replay: 57 fills, no stores", 0.0, (double)ntiles * 57 * 128);
+    // C3's records are contig-major (random within a contig): the tiles of
+    // one contig (64 contigs: ~1850 tiles) read inside its stretch of the two
+    // planes (~2 x 7.8 MB)
+    const uint64_t wl = (2ull * 7800000) / 128;
+    C3Args d{pl, plane / 128, o1, o2, ntiles, 57u, nuc, pep, sink, 1850u, wl};
+    timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, d); },
+           "c3 replay: 57 fills within a contig's planes", (double)ntiles * (nuc + pep),
+           (double)ntiles * 57 * 128);
+    C3Args e{pl, plane / 128, o1, o2, ntiles, 57u, 0u, 0u, sink, 1850u, wl};
+    timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, e); },
+           "c3 replay: 57 fills within a contig, no stores", 0.0, (double)ntiles * 57 * 128);
+  } else {
+    // C5 (profiles/r03_close2): 605,096 tiles; 5.07 GB written per launch
+    // (PMC), reads 1.64 GB; a tile touches ~4 records (six streams each)
+    const uint32_t ntiles = 605096, run = 2096, runs = 4;
+    const uint64_t plane = 1536ull << 20, out = 5ull << 30;
+    uint8_t *pl, *o;
+    CK(hipMalloc(&pl, plane));
+    CK(hipMalloc(&o, out));
+    CK(hipMemset(pl, 1, plane));
+    const size_t pad = lds_pad(reinterpret_cast<const void*>(c5_replay<false, false>), 7);
+    const int grid = (int)((ntiles + 3) / 4);
+    const double wb = (double)ntiles * run * runs, rb = (double)ntiles * 21 * 128;
+    for (uint32_t lines : {0u, 21u}) {
+      C5Args a{pl, plane / 128, o, out / run, ntiles, lines, run, runs, sink, 0u};
+      char nm[96];
+      snprintf(nm, sizeof nm, "c5 replay: %u line fills per tile", lines);
+      timeit([&] { hipLaunchKernelGGL((c5_replay<false, false>), grid, 256, pad, 0, a); }, nm,
+             wb, (double)ntiles * lines * 128);
+    }
+    C5Args a{pl, plane / 128, o, out / run, ntiles, 21u, run, runs, sink, 0u};
+    timeit([&] { hipLaunchKernelGGL((c5_replay<false, true>), grid, 256, pad, 0, a); },
+           "c5 replay: 21 fills, scattered runs, nt", wb, rb);
+    timeit([&] { hipLaunchKernelGGL((c5_replay<true, false>), grid, 256, pad, 0, a); },
+           "c5 replay: 21 fills, sequential runs", wb, rb);
+    timeit([&] { hipLaunchKernelGGL((c5_replay<true, true>), grid, 256, pad, 0, a); },
+           "c5 replay: 21 fills, sequential runs, nt", wb, rb);
+    // the same scattered replay over two more, separately allocated outputs
+    // (is a slow C5 process a property of its allocation?)
+    for (int extra = 0; extra < 2; ++extra) {
+      uint8_t* o2;
+      CK(hipMalloc(&o2, out));
+      C5Args c{pl, plane / 128, o2, out / run, ntiles, 21u, run, runs, sink, 0u};
+      char nm[96];
+      snprintf(nm, sizeof nm, "c5 replay: 21 fills, scattered, buffer %d", extra + 2);
+      timeit([&] { hipLaunchKernelGGL((c5_replay<false, false>), grid, 256, pad, 0, c); }, nm, wb, rb);
+    }
+    timeit([&] { hipLaunchKernelGGL((c5_replay<false, false>), grid, 256, pad, 0, a); },
+           "c5 replay: 21 fills, scattered, buffer 1 again", wb, rb);
+    // runs scattered inside a window of 3000 tiles' output (~25 MB) that
+    // advances with the walk: one contig's records, output in record order,
+    // walked in genome order
+    C5Args b{pl, plane / 128, o, out / run, ntiles, 21u, run, runs, sink, 3000u};
+    timeit([&] { hipLaunchKernelGGL((c5_replay<false, false>), grid, 256, pad, 0, b); },
+           "c5 replay: 21 fills, runs in a moving 25-MB window", wb, rb);
+  }
+  return 0;
+}

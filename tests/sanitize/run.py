@@ -40,7 +40,7 @@ def build():
         obj = os.path.join(BUILD, os.path.basename(src) + '.o')
         subprocess.check_call(['/opt/rocm/bin/hipcc'] + FLAGS + ['-c', src, '-o', obj])
         objs.append(obj)
-    subprocess.check_call(['/opt/rocm/bin/hipcc', '-fsanitize=address,undefined', '-o', EXE] +
+    subprocess.check_call(['/opt/rocm/bin/hipcc', '-fsanitize=address,undefined', '-fno-gpu-sanitize', '-o', EXE] +
                           objs + ['-lpthread'])
     return EXE
 
