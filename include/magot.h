@@ -281,7 +281,10 @@ int magot_codon_symbols(magot_ctx* ctx, const uint8_t* seq, uint64_t n_codons,
  * the REAL codons only: frames 1/2 start with a junk 1-/2-base codon that
  * trimX always drops (genome.py:809-821), so it is not emitted; frame 0 is
  * untrimmed (the caller drops one leading 'X').  Streams start on 16-byte
- * boundaries: stream_off (6n+1) are the padded offsets, stream_len (6n) the
+ * boundaries, a record's three '-' streams before its three '+' streams
+ * (strand-major: the kernel writes each strand's chunks in one pass):
+ * stream_off (6n+1) are the padded offsets (stream_off[6n] the total),
+ * stream_len (6n) the
  * real residue counts, and the padding bytes are 0; none_mask[j] = 1 where
  * the reference returns None (len <= 2 + f).  stream_len / none_mask may be
  * NULL.

@@ -1049,14 +1049,20 @@ int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,
     set_error("magot_orf6_sizes: null argument");
     return MAGOT_ERR_ARG;
   }
+  // A record's streams are placed strand-major: its three '-' streams, then
+  // its three '+' streams.  orf6_kernel writes every '-' chunk of a record
+  // batch before its '+' chunks (strand-uniform chunk passes), so each pass
+  // then stores one contiguous run per record instead of three runs with
+  // gaps the other pass fills later (whose shared 128-B lines leave L2 half
+  // written).
   uint64_t acc = 0;
   for (uint64_t r = 0; r < n; ++r) {
     const uint64_t L = seq_off[r + 1] - seq_off[r];
-    for (uint32_t f = 0; f < 3; ++f) {
-      // real codons start at 2f, 2f+3, ... (frames 1/2 emit a junk codon first)
-      const bool none = L <= 2 + f;
-      const uint64_t c = (!none && L >= 2 * f + 3) ? (L - 2 * f) / 3 : 0;
-      for (int st = 0; st < 2; ++st) {
+    for (int st = 0; st < 2; ++st) {
+      for (uint32_t f = 0; f < 3; ++f) {
+        // real codons start at 2f, 2f+3, ... (frames 1/2 emit a junk codon first)
+        const bool none = L <= 2 + f;
+        const uint64_t c = (!none && L >= 2 * f + 3) ? (L - 2 * f) / 3 : 0;
         const uint64_t j = 6 * r + 2 * f + st;
         stream_off[j] = acc;  // streams start on 16-byte boundaries
         if (stream_len) stream_len[j] = c;

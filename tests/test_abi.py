@@ -50,6 +50,31 @@ def test_translate_sizes_host_function():
     assert poff.tolist() == [0, 0, 0, 1, 2, 5]
 
 
+def test_orf6_sizes_host_function():
+    """Six-frame stream sizes (genome.py:809-818 frame quirk) and placement:
+    16-byte-aligned, non-overlapping spans covering [0, total), each record's
+    three '-' streams (j = 6r + 2f) before its three '+' streams."""
+    lens = [0, 2, 3, 4, 5, 17, 48, 100]
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    n = len(lens)
+    soff = np.empty(6 * n + 1, dtype=np.uint64)
+    slen = np.empty(6 * n, dtype=np.uint64)
+    none = np.empty(6 * n, dtype=np.uint8)
+    _lib.check(_lib.lib().magot_orf6_sizes(_lib.ptr(off), n, _lib.ptr(soff), _lib.ptr(slen),
+                                           _lib.ptr(none)), 'sizes')
+    pos = 0
+    for r, L in enumerate(lens):
+        for st in (0, 1):
+            for f in range(3):
+                j = 6 * r + 2 * f + st
+                want = (L - 2 * f) // 3 if L > 2 + f and L >= 2 * f + 3 else 0
+                assert slen[j] == want, (L, f)
+                assert none[j] == (1 if L <= 2 + f else 0)
+                assert soff[j] == pos
+                pos += (want + 15) & ~15
+    assert soff[6 * n] == pos
+
+
 def test_errors_are_reported_not_swallowed():
     L = _lib.lib()
     rc = L.magot_ctx_create(0, None)
