@@ -135,6 +135,47 @@ __global__ __launch_bounds__(256) void c5_replay(C5Args a) {
   if (acc == 0x12345678u) *a.sink = acc;
 }
 
+// C5 with the staging chain: `chain` dependent load round trips per wave
+// (each round's addresses depend on every lane's previous load, as staging's
+// rows -> windows -> batch offsets do), `lines` fills in all, then the
+// stores.  kSplit: even waves only load (their odd partner's fills too), odd
+// waves only store (their partner's runs too): loads never queue behind the
+// same wave's stores (a producer / consumer split of the staging and chunk
+// phases, without the hand-off).
+template <bool kSplit>
+__global__ __launch_bounds__(256) void c5_chain(C5Args a, uint32_t chain) {
+  const uint32_t xnb = gridDim.x, xb = blockIdx.x;
+  const uint32_t xq = xnb >> 3, xr = xnb & 7, xcd = xb & 7, xk = xb >> 3;
+  const uint32_t vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  const uint64_t w = (uint64_t)vb * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= a.ntiles) return;
+  const bool do_load = !kSplit || (w & 1) == 0, do_store = !kSplit || (w & 1) == 1;
+  const uint32_t lines = kSplit ? 2 * a.lines : a.lines;
+  uint32_t acc = 0, dep = 0;
+  if (do_load) {
+    for (uint32_t k = 0; k < chain; ++k) {
+      const uint32_t l0 = k * lines / chain, l1 = (k + 1) * lines / chain;
+      for (uint32_t l = l0 + lane; l < l1; l += 64) {
+        const uint64_t line = (w * a.lines + l + dep) % a.plane_lines;
+        const uint2 x = *reinterpret_cast<const uint2*>(a.plane + line * 128 + 8 * (l & 15));
+        acc ^= x.x + x.y;
+      }
+      dep = (uint32_t)__ballot(acc == 0x12345u);  // 0, known only once every lane's load is back
+    }
+  }
+  if (do_store) {
+    const uint32_t per = a.run_bytes / 16, runs = kSplit ? 2 * a.runs : a.runs, total = per * runs;
+    const uint64_t wr = (uint64_t)a.win_tiles * a.runs;
+    for (uint32_t q = lane; q < total; q += 64) {
+      const uint32_t r = q / per, c = q - r * per;
+      const uint64_t slot = ((w / a.win_tiles) * wr + mix(w * 64 + r) % wr) % a.out_runs;
+      st16(a.out + slot * a.run_bytes + 16 * c, make_uint4(acc, q, r, (uint32_t)w), false);
+    }
+  }
+  if (acc == 0x12345678u) *a.sink = acc;
+}
+
 // occupancy cap as the product launches use it: dynamic LDS nobody touches
 static size_t lds_pad(const void* fn, int want) {
   int per = 0;
@@ -242,6 +283,21 @@ int main(int argc, char** argv) {
     }
     timeit([&] { hipLaunchKernelGGL((c5_replay<false, false>), grid, 256, pad, 0, a); },
            "c5 replay: 21 fills, scattered, buffer 1 again", wb, rb);
+    if (argc > 2 && !strcmp(argv[2], "chain")) {
+      C5Args b{pl, plane / 128, o, out / run, ntiles, 21u, run, runs, sink, 3000u};
+      const size_t padc = lds_pad(reinterpret_cast<const void*>(c5_chain<false>), 7);
+      for (uint32_t chain : {1u, 3u, 5u}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "c5 chain: %u dependent load rounds", chain);
+        timeit([&] { hipLaunchKernelGGL((c5_chain<false>), grid, 256, padc, 0, b, chain); }, nm, wb, rb);
+        snprintf(nm, sizeof nm, "c5 chain: %u rounds, load/store waves split", chain);
+        timeit([&] { hipLaunchKernelGGL((c5_chain<true>), grid, 256, padc, 0, b, chain); }, nm, wb, rb);
+      }
+      C5Args z{pl, plane / 128, o, out / run, ntiles, 0u, run, runs, sink, 3000u};
+      timeit([&] { hipLaunchKernelGGL((c5_chain<false>), grid, 256, padc, 0, z, 1u); },
+             "c5 chain: stores only (moving window)", wb, 0.0);
+      return 0;
+    }
     // runs scattered inside a window of 3000 tiles' output (~25 MB) that
     // advances with the walk: one contig's records, output in record order,
     // walked in genome order
