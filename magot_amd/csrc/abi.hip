@@ -1271,6 +1271,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   const uint64_t o_t0 = cv.take<uint64_t>(n_tiles + 1);
   const uint64_t o_r0 = cv.take<uint32_t>(n_tiles);
   const uint64_t o_e0 = cv.take<uint32_t>(n_tiles);
+  const uint64_t o_m = cv.take<uint32_t>(n_tiles);
   const uint64_t o_lut = cv.take<uint8_t>(256);
   const uint64_t nib_words = p->args.span / 4;  // forward + reverse planes, 8 bases per word
   const uint64_t code2_words = nib_words / 2;
@@ -1294,6 +1295,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   MAGOT_HIP_TRY(up(o_t0, tiles.t0.data(), (n_tiles + 1) * 8));
   MAGOT_HIP_TRY(up(o_r0, tiles.r0.data(), n_tiles * 4));
   MAGOT_HIP_TRY(up(o_e0, tiles.e0.data(), n_tiles * 4));
+  MAGOT_HIP_TRY(up(o_m, tiles.m.data(), n_tiles * 4));
   MAGOT_HIP_TRY(up(o_lut, tables, 256));
   o->out = reinterpret_cast<uint8_t*>(base + o_out);
   Orf6Args& a = o->args;
@@ -1312,6 +1314,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   a.tile_t0 = reinterpret_cast<const uint64_t*>(base + o_t0);
   a.tile_r0 = reinterpret_cast<const uint32_t*>(base + o_r0);
   a.tile_e0 = reinterpret_cast<const uint32_t*>(base + o_e0);
+  a.tile_m = reinterpret_cast<const uint32_t*>(base + o_m);
   a.n_tiles = n_tiles;
   a.tables = reinterpret_cast<const uint8_t*>(base + o_lut);
   a.out = o->out;

@@ -239,13 +239,14 @@ struct Orf6Args {
   const uint64_t* tile_t0;
   const uint32_t* tile_r0;
   const uint32_t* tile_e0;
+  const uint32_t* tile_m;  // rows of the tile's window (interval starts before its end), <= kOrf6RowCap
   uint64_t n_tiles;
   const uint8_t* tables;  // 256 bytes from orf6_tables
   uint8_t* out;
 };
 struct Orf6Tiles {
   std::vector<uint64_t> t0;
-  std::vector<uint32_t> r0, e0;
+  std::vector<uint32_t> r0, e0, m;
 };
 void orf6_tables(const uint8_t lut64[64], uint8_t out[256]);
 void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_start,

@@ -463,13 +463,17 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     uint4* const row = reinterpret_cast<uint4*>(s_scratch[wave]);
     uint32_t* const cnt = codes;  // 256 counters, then the vector -> interval map
     const uint64_t e0 = a.tile_e0[tile];
+    const uint32_t mrow = a.tile_m[tile];
     const int32_t wlen = (int32_t)(WE - W0);
     int32_t rel[2];
     bool in[2];
     ulonglong2 rw[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // sentinel row n_rows
-      const uint64_t j = min(e0 + (uint64_t)(lane + 64 * h), a.n_rows);
+    for (int h = 0; h < 2; ++h) {
+      // rows e0 .. e0 + m (the window's intervals, then the first one past
+      // its end); the other lanes load row m again, so a wave fetches the
+      // lines of its ~30 rows instead of 128 rows (sentinel row n_rows)
+      const uint64_t j = min(e0 + min((uint32_t)(lane + 64 * h), mrow), a.n_rows);
       rw[h] = *reinterpret_cast<const ulonglong2*>(a.rows + 2 * j);
     }
 #pragma unroll
@@ -803,7 +807,8 @@ void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_s
   out->t0.clear();
   out->r0.clear();
   out->e0.clear();
-  uint64_t r = 0, e = 0;
+  out->m.clear();
+  uint64_t r = 0, e = 0, f = 0;
   for (uint64_t T = 0; T < total;) {
     const uint64_t W0 = (T >= 48 ? T - 48 : 0) & ~15ull;
     while (r + 1 < n_rec && noff[r + 1] <= T) ++r;  // the record holding base T
@@ -816,6 +821,12 @@ void orf6_plan_tiles(const uint64_t* noff, uint64_t n_rec, const uint64_t* row_s
         if (T1 + 50 > cap) T1 = std::max(T + 1, cap - 50);
       }
       out->e0.push_back((uint32_t)e);
+      // the window's rows: intervals starting before its end (the kernel
+      // loads rows e .. e + m, the last one the sentinel)
+      const uint64_t WE = std::min(T1 + 50, total);
+      f = std::max(f, e);
+      while (f < n_rows && row_start[f] < WE) ++f;
+      out->m.push_back((uint32_t)std::min<uint64_t>(f - e, kOrf6RowCap));
     }
     out->t0.push_back(T);
     out->r0.push_back((uint32_t)r);
