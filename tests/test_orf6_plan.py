@@ -66,3 +66,6 @@ def test_upper_lane_workload_reaches_the_case():
     wins = orf6_windows(upper_lane_workload())
     assert upper_only(wins) >= 20
     assert max(m for _, m, _ in wins) > 64          # rows staged by both lane halves
+    # the kernel stages rows e .. e + m (tile_m, capped at ROW_CAP; the last
+    # one the sentinel past the window): the cap never cuts a window here
+    assert max(m for _, m, _ in wins) <= ROW_CAP
