@@ -143,7 +143,7 @@ __global__ __launch_bounds__(256) void c5_replay(C5Args a) {
 // same wave's stores (a producer / consumer split of the staging and chunk
 // phases, without the hand-off).
 template <bool kSplit>
-__global__ __launch_bounds__(256) void c5_chain(C5Args a, uint32_t chain) {
+__global__ __launch_bounds__(256) void c5_chain(C5Args a, uint32_t chain, uint32_t extra) {
   const uint32_t xnb = gridDim.x, xb = blockIdx.x;
   const uint32_t xq = xnb >> 3, xr = xnb & 7, xcd = xb & 7, xk = xb >> 3;
   const uint32_t vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
@@ -160,6 +160,13 @@ __global__ __launch_bounds__(256) void c5_chain(C5Args a, uint32_t chain) {
         const uint64_t line = (w * a.lines + l + dep) % a.plane_lines;
         const uint2 x = *reinterpret_cast<const uint2*>(a.plane + line * 128 + 8 * (l & 15));
         acc ^= x.x + x.y;
+      }
+      // `extra` more load instructions per round over the same lines (L2
+      // hits: staging's row, table, window and offset loads)
+      for (uint32_t x = 0; x < extra; ++x) {
+        const uint64_t line = (w * a.lines + ((lane + x) % a.lines) + dep) % a.plane_lines;
+        const uint2 y = *reinterpret_cast<const uint2*>(a.plane + line * 128 + 8 * ((lane + x) & 15));
+        acc ^= y.x + y.y;
       }
       dep = (uint32_t)__ballot(acc == 0x12345u);  // 0, known only once every lane's load is back
     }
@@ -289,12 +296,17 @@ int main(int argc, char** argv) {
       for (uint32_t chain : {1u, 3u, 5u}) {
         char nm[96];
         snprintf(nm, sizeof nm, "c5 chain: %u dependent load rounds", chain);
-        timeit([&] { hipLaunchKernelGGL((c5_chain<false>), grid, 256, padc, 0, b, chain); }, nm, wb, rb);
+        timeit([&] { hipLaunchKernelGGL((c5_chain<false>), grid, 256, padc, 0, b, chain, 0u); }, nm, wb, rb);
         snprintf(nm, sizeof nm, "c5 chain: %u rounds, load/store waves split", chain);
-        timeit([&] { hipLaunchKernelGGL((c5_chain<true>), grid, 256, padc, 0, b, chain); }, nm, wb, rb);
+        timeit([&] { hipLaunchKernelGGL((c5_chain<true>), grid, 256, padc, 0, b, chain, 0u); }, nm, wb, rb);
+      }
+      for (uint32_t extra : {3u, 6u}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "c5 chain: 5 rounds + %u L2-hit load insts each", extra);
+        timeit([&] { hipLaunchKernelGGL((c5_chain<false>), grid, 256, padc, 0, b, 5u, extra); }, nm, wb, rb);
       }
       C5Args z{pl, plane / 128, o, out / run, ntiles, 0u, run, runs, sink, 3000u};
-      timeit([&] { hipLaunchKernelGGL((c5_chain<false>), grid, 256, padc, 0, z, 1u); },
+      timeit([&] { hipLaunchKernelGGL((c5_chain<false>), grid, 256, padc, 0, z, 1u, 0u); },
              "c5 chain: stores only (moving window)", wb, 0.0);
       return 0;
     }
