@@ -16,7 +16,13 @@
 //     their output offsets), plain 16-B stores, one store per lane per
 //     pass as orf6_kernel's chunk loop; L line fills per wave from a 1.5-GB
 //     code plane, walked in genome order (neighbouring tiles read
-//     neighbouring lines).
+//     neighbouring lines).  Variants: runs written sequentially (the
+//     record-order walk), inside a moving 25-MB window (one contig's records,
+//     genome-order walk), scattered over the whole output.
+// c5 chain: the same stores after 1, 3 or 5 dependent load round trips per
+//     wave (staging's shape), with loads and stores in the same or in
+//     separate waves, and with extra load instructions per round.
+//   usage: solbench c3 | solbench c5 [chain]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
