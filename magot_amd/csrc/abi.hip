@@ -567,7 +567,10 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
       uint64_t T1 = std::min<uint64_t>(T0 + tile, B);
       if (e1 + kExonCap < Ec) T1 = std::min<uint64_t>(T1, ex_out[e1 + kExonCap] - kHalo);
       if (j1 + kTxCap - kChunk < Tc) T1 = std::min<uint64_t>(T1, tn[j1 + kTxCap - kChunk]);
-      if (T1 < B) T1 &= ~(uint64_t)(kChunk - 1);
+      // cut on a 128-byte line boundary where the tile keeps one (no
+      // nucleotide line is then written by two tiles), else on a chunk
+      if (T1 < B) T1 = (T1 & ~(uint64_t)(kTileAlign - 1)) > T0 ? T1 & ~(uint64_t)(kTileAlign - 1)
+                                                             : T1 & ~(uint64_t)(kChunk - 1);
       if (T1 < T0 + kChunk) T1 = std::min<uint64_t>(T0 + kChunk, B);
       const uint64_t dec_end = std::min<uint64_t>(T1 + kHalo, B);
       // residues owned: every codon starting before T1, rounded up to a chunk,

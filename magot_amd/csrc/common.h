@@ -94,6 +94,11 @@ constexpr int kTile = (kSlots - 3) * kChunk;    // 5072 output bytes per tile (3
 constexpr int tile_bytes(int lane_chunks) { return (64 * lane_chunks - 3) * 16; }
 // plans whose large-tile count is below this use the small tile
 constexpr uint64_t kSmallTilePlan = 40000;
+// extraction tiles end on this output boundary where they can (bytes)
+#ifndef MAGOT_EXP_TILE_ALIGN
+#define MAGOT_EXP_TILE_ALIGN 128
+#endif
+constexpr uint64_t kTileAlign = MAGOT_EXP_TILE_ALIGN;
 constexpr int kPepPerLane = 2;                // residue chunk slots per lane
 constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
                                               // the residues rounded up to a 16-byte store

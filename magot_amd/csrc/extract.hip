@@ -518,9 +518,10 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   const uint64_t T0 = d.T0;
 
   // Chunks at tile bytes p < edge_lo or p >= edge_hi lie in the 128-byte lines
-  // the tile shares with its neighbours (plain stores there, store16_edge).
-  const int edge_lo = (int)((((T0 >> 7) + 1) << 7) - T0);
-  const int edge_hi = (int)((((d.T1 - 1) >> 7) << 7) - T0);
+  // the tile shares with its neighbours (plain stores there, store16_edge);
+  // a tile boundary on a line boundary shares none (the planner cuts there).
+  const int edge_lo = (int)((((T0 + 127) >> 7) << 7) - T0);
+  const int edge_hi = (int)(((d.T1 >> 7) << 7) - T0);
 
   // ---- nucleotide chunks: issue every window load first -------------------
   const __amdgpu_buffer_rsrc_t nib_rs = plane_rsrc(a.nib);
