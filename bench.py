@@ -47,7 +47,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
-CONFIGS = ['C2', 'C3', 'C5', 'small']
+CONFIGS = ['C2', 'C3', 'C5', 'small', 'small5']
 
 
 def log(msg):
@@ -144,7 +144,8 @@ def shard_seed(config, rank):
     """Seed of rank `rank`'s weak-scaling job: SURVEY 8(d) seed for rank 0,
     +1000 per rank (strong mode: every rank uses rank 0's)."""
     from magot_amd import synth
-    return synth.SEED_BASE + {'C2': 2, 'C3': 3, 'C5': 5, 'small': 9}[config] + 1000 * rank
+    return synth.SEED_BASE + {'C2': 2, 'C3': 3, 'C5': 5, 'small': 9, 'small5': 9}[config] + \
+        1000 * rank
 
 
 def barrier(dist):
@@ -350,6 +351,8 @@ _DESC = {
     'C5': '3 Gb genome (200 lognormal contigs), 2M transcripts; CDS gather + six-frame '
           'translation (get_orfs)',
     'small': '1 Mb genome (8 contigs), 500 transcripts (test size); nucleotide + peptide out',
+    'small5': '1 Mb genome (8 contigs), 500 transcripts (test size); six-frame translation '
+              '(the C5 job at test size)',
 }
 
 
@@ -372,16 +375,16 @@ def run_job(args, dist, rank, local, world):
 
     from magot_amd import _lib, engine, shard, synth
     strong = args.mode == 'strong'
-    c5 = args.config == 'C5'
-    t0 = time.perf_counter()
-    w = synth.make(args.config, seed=shard_seed(args.config, 0 if strong else rank),
-                   order=args.order)
+    c5 = args.config in ('C5', 'small5')
+    t_start = t0 = time.perf_counter()
+    w = synth.make('small' if args.config == 'small5' else args.config,
+                   seed=shard_seed(args.config, 0 if strong else rank), order=args.order)
     t_gen = time.perf_counter() - t0
     log('generated %s: %d contigs, %d transcripts, %d exons, %d CDS bases (%.1fs)'
         % (args.config, len(w.contig_len), w.n_tx, w.n_exons, w.cds_bases, t_gen))
     ctx = _lib.Context(local)
 
-    mine, imb, t_bcast, t_pack = None, 0.0, None, None
+    mine, imb, t_bcast, t_pack, bcast_bytes = None, 0.0, None, None, None
     shards = None
     rehearse = None
     if args.rehearse_shard and world == 1:
@@ -405,7 +408,8 @@ def run_job(args, dist, rank, local, world):
         imb = shard.imbalance(load)
         log('%d records over %d ranks: load imbalance %.4f%%, %d contig(s) split'
             % (w.n_tx, world, 100.0 * imb, int((spans[:, 0] != spans[:, 1]).sum())))
-        dev, t_bcast = shard.replicate_genome(dist, rank, w.contigs() if rank == 0 else None, ctx)
+        dev, t_bcast, bcast_bytes = shard.replicate_genome(
+            dist, rank, w.contigs() if rank == 0 else None, ctx)
         t_bcast = allreduce_max(dist, t_bcast)
     else:
         t0 = time.perf_counter()
@@ -436,9 +440,12 @@ def run_job(args, dist, rank, local, world):
         kernel_name = 'extract_kernel'
         step = plan.execute
 
+    t_setup = time.perf_counter() - t_start
     # -- correctness of the measured configuration (each rank, its own shard) -----
     parity = 'not checked'
+    launches_before = 0  # launches of the measured kernel before the timed steps
     if not args.no_verify:
+        launches_before += 1
         t0 = time.perf_counter()
         ok = verify_orf6(w, plan, o6, mine) if c5 else verify_extract(w, plan, mine)
         log('rank-local parity %s (%.1fs)' % ('ok' if ok else 'MISMATCH', time.perf_counter() - t0))
@@ -450,25 +457,29 @@ def run_job(args, dist, rank, local, world):
 
     # -- timed region ---------------------------------------------------------
     settled = settle(step, ctx.sync, args.settle_ms)
+    launches_before += settled['launches'] + args.warmup
     for _ in range(args.warmup):
         step()
     ctx.sync()
     barrier(dist)
     ctx.sync()
     t0 = time.perf_counter()
+    ctx.mark(0)
     for _ in range(args.steps):
         step()
+    ctx.mark(1)
     ctx.sync()
     elapsed = time.perf_counter() - t0
     barrier(dist)
     elapsed_max = allreduce_max(dist, elapsed)
 
     # per-launch kernel duration from HIP events on the context stream (the
-    # kernel's own stream): one event pair around back-to-back launches, as
-    # the steps run; the isolated-launch mean is reported beside it
+    # kernel's own stream) around exactly the K timed launches; back-to-back
+    # and isolated launches after the timed region are reported beside it
     timer = o6 if c5 else plan
+    kernel_ms = ctx.elapsed_ms() / args.steps
     n_b2b = max(20, min(args.steps, 100))
-    kernel_ms = timer.time_b2b(n_b2b)
+    kernel_b2b = timer.time_b2b(n_b2b)
     kernel_iso = timer.time(10)
     kernel_ms_max = allreduce_max(dist, kernel_ms)
     total_bases = allreduce_sum(dist, float(B))
@@ -494,8 +505,15 @@ def run_job(args, dist, rank, local, world):
     phases['outputs_d2h_pinned'] = t_d2h
     del pin
     gather = None
-    if world > 1 and strong and not c5:
-        gather = gather_outputs(args, dist, rank, world, w, plan, shards)
+    if world > 1 and strong:
+        gather = gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx)
+    import resource
+    rss_gb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2.0 ** 20  # KiB -> GiB
+    host = {'peak_rss_gib_max_rank': allreduce_max(dist, rss_gb),
+            'peak_rss_gib_rank0': rss_gb,
+            'setup_s_max_rank': allreduce_max(dist, t_setup),
+            'setup': 'workload generation + genome pack or broadcast + plan upload, before '
+                     'the parity check'}
 
     # -- roofline / traffic / baselines --------------------------------------------
     traffic = None
@@ -546,9 +564,17 @@ def run_job(args, dist, rank, local, world):
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'kernel': kernel_name, 'kernel_ms': kernel_ms_max,
-                         'kernel_ms_source': 'HIP events around %d back-to-back launches on '
-                                             'the kernel\'s stream (max over ranks)' % n_b2b,
+                         'kernel_ms_source': 'HIP events on the kernel\'s stream around the K '
+                                             'timed launches, / K (max over ranks)',
+                         'kernel_ms_b2b': kernel_b2b,
+                         'kernel_ms_b2b_source': 'HIP events around %d back-to-back launches '
+                                                 'after the timed region' % n_b2b,
                          'kernel_ms_isolated': kernel_iso,
+                         'timed_launches': {'kernel': kernel_name, 'first': launches_before,
+                                            'count': args.steps,
+                                            'note': 'dispatch indices of this kernel in the '
+                                                    'process (0-based): the K timed launches '
+                                                    '(scripts/rocprof_summary.py --timed)'},
                          'rocprof_kernel_ms': rp['avg_ms'] if rp else None,
                          'rocprof_frac': (alg_mean / (rp['avg_ms'] * 1e-3) / 1e9 / HBM_PEAK_GBS)
                          if rp else None,
@@ -559,6 +585,7 @@ def run_job(args, dist, rank, local, world):
             'settle': settled, 'device': ctx.info(),
             'parity': parity,
             'phases_s': phases,
+            'host': host,
             'outputs_d2h_bases_per_s': total_bases / t_d2h if t_d2h else None,
             'output_bytes_rank0': out_bytes,
         }
@@ -568,6 +595,8 @@ def run_job(args, dist, rank, local, world):
                 '%s job on one GPU' % (rehearse['rank'], rehearse['ranks'], args.config)
         if strong and world > 1:
             rec['genome_broadcast_s'] = t_bcast
+            rec['genome_broadcast_bytes'] = bcast_bytes
+            rec['genome_arena_bytes'] = int(dev.device_bytes)
             rec['load_imbalance'] = imb
             rec['outputs_gather'] = gather
         print(json.dumps(rec), flush=True)
@@ -579,47 +608,77 @@ def run_job(args, dist, rank, local, world):
         dist.destroy_process_group()
 
 
-def gather_outputs(args, dist, rank, world, w, plan, shards):
+def gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx):
     """Every rank's outputs to rank 0 over the collective backend (device to
-    device with RCCL), once, timed; rank 0 restores global record order and
-    (unless --no-verify) checks the whole job against the oracle."""
+    device with RCCL), once, timed; rank 0 puts them back into global record
+    order on the device (one magot_copy_segments launch, timed) and, unless
+    --no-verify, checks the whole job against the oracle.  C3: nucleotides
+    and peptides, per-record segments; C5: the six-frame streams, one segment
+    per record (a record's six padded streams are contiguous, in the same
+    layout as the single-GPU job: magot_orf6_sizes over the global order)."""
     import torch
 
     from magot_amd import engine, shard
-    B, P = plan.nuc_bytes, plan.pep_bytes
-    gn = shard.Gather(dist, rank, world, B)
-    gp = shard.Gather(dist, rank, world, P) if plan.outputs & engine.OUT_PEP else None
-    plan.execute()
-    plan.copy_outputs(gn.send.data_ptr(), gp.send.data_ptr() if gp is not None and P else None)
+    items = []  # (name, bytes, copy to device address, record offsets)
+    if o6 is not None:
+        soff, _ = o6.fetch_to(None)
+        items.append(('six-frame residues', o6.total, o6.copy_outputs,
+                      np.append(soff[0:-1:6], soff[-1]).astype(np.int64)))
+    else:
+        _, noff, _, poff = plan.fetch()
+        items.append(('nucleotides', plan.nuc_bytes,
+                      lambda a: plan.copy_outputs(a, None), noff.astype(np.int64)))
+        if plan.outputs & engine.OUT_PEP:
+            items.append(('peptides', plan.pep_bytes,
+                          lambda a: plan.copy_outputs(None, a), poff.astype(np.int64)))
+    gathers = [shard.Gather(dist, rank, world, nb) for _, nb, _, _ in items]
+    for g, (_, nb, copy, _) in zip(gathers, items):
+        if nb:
+            copy(g.send.data_ptr())
     torch.cuda.synchronize()
     barrier(dist)
     t0 = time.perf_counter()
-    gn.run()
-    if gp is not None:
-        gp.run()
+    for g in gathers:
+        g.run()
     torch.cuda.synchronize()
     t_gather = allreduce_max(dist, time.perf_counter() - t0)
-    _, noff, _, poff = plan.fetch()
-    offs = [None] * world
-    dist.gather_object((noff.tolist(), poff.tolist()), offs if rank == 0 else None, dst=0)
-    res = {'seconds': t_gather, 'bytes': int(allreduce_sum(dist, float(B + P))),
-           'backend': dist.get_backend()}
-    if rank == 0:
-        g_nuc = gn.parts()
-        g_pep = gp.parts() if gp is not None else None
-        check = 'not checked'
-        if not args.no_verify:
-            from oracle import cds_oracle
-            nuc, goff = shard.reassemble(shards, g_nuc, [o[0] for o in offs])
-            ref, roff, st = cds_oracle.extract_workload(w, False)
-            ok = (not st.any()) and np.array_equal(nuc, ref) and np.array_equal(goff, roff)
-            if ok and g_pep is not None:
-                pep, pgoff = shard.reassemble(shards, g_pep, [o[1] for o in offs])
+    offs = [shard.gather_offsets(dist, rank, world, off) for _, _, _, off in items]
+    res = {'seconds': t_gather, 'bytes': int(allreduce_sum(dist, float(sum(it[1] for it in items)))),
+           'backend': dist.get_backend(), 'outputs': [it[0] for it in items]}
+    if rank != 0:
+        return res
+    t0 = time.perf_counter()
+    glob = []
+    for g, off in zip(gathers, offs):
+        glob.append(shard.reassemble_device(shards, off, g.received(), g.cap, ctx=ctx))
+    torch.cuda.synchronize()
+    res['reassembly_s'] = time.perf_counter() - t0
+    res['reassembly'] = 'magot_copy_segments on rank 0\'s device: %d records into global order' \
+        % w.n_tx
+    check = 'not checked'
+    if not args.no_verify:
+        from oracle import cds_oracle
+        ref, roff, st = cds_oracle.extract_workload(w, False)
+        ok = not st.any()
+        if o6 is not None:
+            out, goff = glob[0]
+            soff, slen = engine.orf6_sizes(roff)
+            ok = ok and np.array_equal(goff, soff[0::6].astype(np.int64))
+            if ok:
+                bad, first = cds_oracle.orf6_compare(ref, roff, out.cpu().numpy(), soff, slen,
+                                                     threads=host_threads())
+                ok = bad == 0
+        else:
+            nuc, goff = glob[0]
+            ok = ok and np.array_equal(nuc.cpu().numpy(), ref) and np.array_equal(goff, roff)
+            if ok and len(glob) > 1:
+                pep, pgoff = glob[1]
                 pref, _, _ = cds_oracle.extract_workload(w, True)
-                ok = _pep_matches(pep, pgoff, pref)
-            check = 'bit-exact vs CPU oracle (gathered, global record order)' if ok \
-                else 'MISMATCH'
-        res['parity'] = check
+                ok = _pep_matches(pep.cpu().numpy(), pgoff, pref)
+        check = ('bit-exact vs CPU oracle (gathered, global record order%s)'
+                 % (', all six frames of every record' if o6 is not None else '')) if ok \
+            else 'MISMATCH'
+    res['parity'] = check
     return res
 
 

@@ -108,6 +108,18 @@ void magot_ctx_destroy(magot_ctx* ctx);
 int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
                       uint32_t n_contigs, magot_genome** out);
 /*
+ * The same with flags.  By default (and in magot_genome_load /
+ * magot_genome_load_fasta) the packing runs on the device: the raw bytes are
+ * streamed into HBM once through pinned buffers and kernels build the nibble
+ * plane, its mirror and the exception runs (the run list's directory is built
+ * on the host from the runs).  MAGOT_PACK_HOST packs on the host (pack.cpp,
+ * the sanitizer-tested twin) and uploads the plane; both give the same arena
+ * bytes (tests/test_gpu_replication.py).
+ */
+#define MAGOT_PACK_HOST 1u
+int magot_genome_load_ex(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
+                         uint32_t n_contigs, uint32_t flags, magot_genome** out);
+/*
  * Read FASTA text (GenomeSequence, genome.py:854-877, incl. truncate_names)
  * natively and pack it like magot_genome_load (MAGOT_ERR_UNSUPPORTED above
  * one device plane, as there).  MAGOT_ERR_UNSUPPORTED also for
@@ -170,6 +182,31 @@ int magot_genome_export(const magot_genome* g, uint8_t* meta, uint64_t cap, uint
 int magot_genome_copy_arena(const magot_genome* g, void* dst_dev);
 int magot_genome_attach(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len, void* arena_dev,
                         magot_genome** out);
+/*
+ * What a replica must receive: magot_genome_wire_ranges gives the *n (= 2)
+ * byte ranges [off[k], off[k]+len[k]) of the arena to transfer -- the forward
+ * nibble plane (span/2 bytes), then the exception runs and their directory.
+ * The reverse-strand mirror between them (as many bytes again) is a pure
+ * function of the forward plane (genome.py:784-793), so
+ * magot_genome_attach_wire attaches like magot_genome_attach and then rebuilds
+ * the mirror on the receiving device: half the bytes cross xGMI.  The caller
+ * memory must be arena_bytes long and hold the wire ranges at their offsets.
+ */
+int magot_genome_wire_ranges(const magot_genome* g, uint64_t* off, uint64_t* len, uint32_t* n);
+int magot_genome_attach_wire(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len,
+                             void* arena_dev, magot_genome** out);
+
+/*
+ * Reassembly of a sharded job's outputs on one device (outputs
+ * gathered back, final order restored from the global record index): for
+ * i < n, dst[dst_off[i], dst_off[i+1]) = src[src_off[i], src_off[i] +
+ * dst_off[i+1] - dst_off[i]).  src and dst are device memory (e.g. the buffer
+ * an RCCL gather filled, rank-major), dst_off has n+1 non-decreasing entries,
+ * the offset tables are host arrays.  Synchronous.  No reference counterpart
+ * (the reference is single-process).
+ */
+int magot_copy_segments(magot_ctx* ctx, const void* src_dev, void* dst_dev, const uint64_t* src_off,
+                        const uint64_t* dst_off, uint64_t n);
 
 /*
  * Build a device-resident plan: interval table -> output offsets, ~3 KiB
@@ -189,6 +226,13 @@ int magot_plan_execute(magot_ctx* ctx, magot_plan* p);
 
 /* Block until the context stream is idle. */
 int magot_ctx_sync(magot_ctx* ctx);
+
+/* Timing marks on the context stream: magot_ctx_mark(ctx, 0) and (ctx, 1)
+ * record events before and after a region of enqueued work (e.g. bench.py's
+ * K timed steps); magot_ctx_elapsed waits for mark 1 and gives the GPU time
+ * between them in ms.  No reference counterpart (measurement). */
+int magot_ctx_mark(magot_ctx* ctx, int which);
+int magot_ctx_elapsed(magot_ctx* ctx, double* ms);
 
 /* Device facts of a context: compute units, and the extraction kernel's
  * resident workgroups per CU as launched (its occupancy cap included).  Any
@@ -253,8 +297,10 @@ int magot_translate_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* s
  * Single-sequence forms of the two (the SURVEY 8(b) sketch), same semantics.
  * magot_revcomp: out holds len bytes.  magot_translate: standard code, frame
  * >= 0 (MAGOT_ERR_UNSUPPORTED below: the Python layer lays negative frames out
- * itself), strand '+' or '-', trimX 0/1; out holds len/3 bytes; *out_len =
- * residues written, or -1 where the reference returns None.
+ * itself), strand '+' or '-', trimX 0/1; out must hold (len + 2) / 3 bytes
+ * (frames 1 and 2 emit a junk first codon: frame 1 of a length with len % 3
+ * == 2 gives (len + 1) / 3 residues before the trim); exactly *out_len bytes
+ * are written; *out_len = residues, or -1 where the reference returns None.
  */
 int magot_revcomp(magot_ctx* ctx, const uint8_t* seq, uint64_t len, uint8_t* out);
 int magot_translate(magot_ctx* ctx, const uint8_t* seq, uint64_t len, int frame, int strand,
@@ -284,10 +330,13 @@ int magot_codon_symbols(magot_ctx* ctx, const uint8_t* seq, uint64_t n_codons,
  * boundaries, a record's three '-' streams before its three '+' streams
  * (strand-major: the kernel writes each strand's chunks in one pass):
  * stream_off (6n+1) are the padded offsets (stream_off[6n] the total),
- * stream_len (6n) the
- * real residue counts, and the padding bytes are 0; none_mask[j] = 1 where
- * the reference returns None (len <= 2 + f).  stream_len / none_mask may be
- * NULL.
+ * stream_len (6n) the real residue counts, and the padding bytes are 0;
+ * none_mask[j] = 1 where the reference returns None (len <= 2 + f).  Because
+ * of the strand-major placement stream_off[j+1] is NOT where stream j's
+ * padding ends: stream j occupies [stream_off[j], stream_off[j] +
+ * pad16(stream_len[j])), pad16(x) = (x + 15) & ~15, and a record's six streams
+ * are one contiguous block [stream_off[6r], stream_off[6r+6]).  Callers that
+ * need the extents must pass stream_len; none_mask may be NULL.
  */
 int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,
                      uint64_t* stream_len, uint8_t* none_mask);
@@ -303,6 +352,9 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
 int magot_orf6_execute(magot_ctx* ctx, magot_orf6* o);
 int magot_orf6_fetch(magot_ctx* ctx, magot_orf6* o, uint8_t* out, uint64_t* stream_off,
                      uint64_t* stream_len);
+/* D2D copy of the padded residue bytes (total_res) into caller device memory
+ * (e.g. the buffer an output gather sends). */
+int magot_orf6_copy_outputs(magot_ctx* ctx, magot_orf6* o, void* dst_dev);
 int magot_orf6_time(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms);
 int magot_orf6_time_b2b(magot_ctx* ctx, magot_orf6* o, int iters, double* avg_ms);
 void magot_orf6_destroy(magot_orf6* o);

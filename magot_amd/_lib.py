@@ -41,6 +41,8 @@ EXPORTS = (
     'magot_genome_load_fasta', 'magot_genome_contigs', 'magot_fasta_read',
     'magot_fasta_text_create', 'magot_fasta_text_execute', 'magot_fasta_text_fetch',
     'magot_fasta_text_time', 'magot_fasta_text_destroy',
+    'magot_genome_load_ex', 'magot_genome_wire_ranges', 'magot_genome_attach_wire',
+    'magot_copy_segments', 'magot_ctx_mark', 'magot_ctx_elapsed', 'magot_orf6_copy_outputs',
 )
 
 ERR_UNSUPPORTED = -5
@@ -49,6 +51,7 @@ GFF_ORDER_PY2 = 2
 GFF_LONGEST = 4
 GFF_GENOMIC = 8
 GFF_FROM_EXONS = 16
+PACK_HOST = 1
 
 
 class MagotError(RuntimeError):
@@ -139,6 +142,16 @@ def _declare(lib):
                                                    ctypes.c_int, ctypes.POINTER(_vp)]),
         'magot_genome_contigs': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_uint32), _vp, _vp,
                                                 ctypes.c_uint64, _u64p]),
+        'magot_genome_load_ex': (ctypes.c_int, [_vp, ctypes.POINTER(_u8p), _u64p, ctypes.c_uint32,
+                                                ctypes.c_uint32, ctypes.POINTER(_vp)]),
+        'magot_genome_wire_ranges': (ctypes.c_int, [_vp, _u64p, _u64p,
+                                                    ctypes.POINTER(ctypes.c_uint32)]),
+        'magot_genome_attach_wire': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp,
+                                                    ctypes.POINTER(_vp)]),
+        'magot_copy_segments': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64]),
+        'magot_ctx_mark': (ctypes.c_int, [_vp, ctypes.c_int]),
+        'magot_orf6_copy_outputs': (ctypes.c_int, [_vp, _vp, _vp]),
+        'magot_ctx_elapsed': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),
         'magot_fasta_read': (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_int,
                                             ctypes.POINTER(ctypes.c_uint32), _vp, _vp,
                                             ctypes.c_uint64, _u64p, _vp, ctypes.c_uint64]),
@@ -191,6 +204,17 @@ class Context(object):
 
     def sync(self):
         check(lib().magot_ctx_sync(self.handle), 'magot_ctx_sync')
+
+    def mark(self, which):
+        """Record timing event `which` (0 = start, 1 = end) on the context
+        stream (magot_ctx_mark)."""
+        check(lib().magot_ctx_mark(self.handle, int(which)), 'magot_ctx_mark')
+
+    def elapsed_ms(self):
+        """GPU time between marks 0 and 1 (waits for mark 1)."""
+        ms = ctypes.c_double()
+        check(lib().magot_ctx_elapsed(self.handle, ctypes.byref(ms)), 'magot_ctx_elapsed')
+        return ms.value
 
     def info(self):
         """{'n_cu', 'extract_blocks_per_cu'} of the device (magot_ctx_info)."""

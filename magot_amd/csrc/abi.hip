@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <thread>
 
 #include "common.h"
 
@@ -40,6 +41,10 @@ struct magot_ctx {
   int blocks_per_cu = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t mark0 = nullptr, mark1 = nullptr;  // magot_ctx_mark
+  // pinned staging ring for genome uploads (allocated on first use)
+  uint8_t* pin[2] = {nullptr, nullptr};
+  hipEvent_t pin_ev[2] = {nullptr, nullptr};
 };
 
 struct magot_genome {
@@ -153,8 +158,10 @@ std::vector<uint8_t> genome_meta(const magot_genome* g) {
   return w.buf;
 }
 
-// Pack the contigs on the host and upload the planes (magot_genome_load*).
-int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, magot_genome** out);
+// Pack the contigs and place the planes in HBM (magot_genome_load*): on the
+// device by default, on the host (pack.cpp) with MAGOT_PACK_HOST.
+int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, uint32_t flags,
+                magot_genome** out);
 
 }  // namespace
 
@@ -189,6 +196,8 @@ int magot_ctx_create(int device, magot_ctx** out) {
   MAGOT_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   MAGOT_HIP_TRY(hipEventCreate(&c->ev0));
   MAGOT_HIP_TRY(hipEventCreate(&c->ev1));
+  MAGOT_HIP_TRY(hipEventCreate(&c->mark0));
+  MAGOT_HIP_TRY(hipEventCreate(&c->mark1));
   MAGOT_HIP_TRY(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
   c->blocks_per_cu = extract_blocks_per_cu();
   *out = c.release();
@@ -201,6 +210,12 @@ void magot_ctx_destroy(magot_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->mark0) (void)hipEventDestroy(ctx->mark0);
+  if (ctx->mark1) (void)hipEventDestroy(ctx->mark1);
+  for (int k = 0; k < 2; ++k) {
+    if (ctx->pin_ev[k]) (void)hipEventDestroy(ctx->pin_ev[k]);
+    if (ctx->pin[k]) (void)hipHostFree(ctx->pin[k]);
+  }
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -221,11 +236,38 @@ int magot_ctx_sync(magot_ctx* ctx) {
   return MAGOT_OK;
 }
 
-int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
-                      uint32_t n_contigs, magot_genome** out) {
+int magot_ctx_mark(magot_ctx* ctx, int which) {
+  if (int rc = bind(ctx)) return rc;
+  if (which != 0 && which != 1) {
+    set_error("magot_ctx_mark: which must be 0 or 1");
+    return MAGOT_ERR_ARG;
+  }
+  MAGOT_HIP_TRY(hipEventRecord(which ? ctx->mark1 : ctx->mark0, ctx->stream));
+  return MAGOT_OK;
+}
+
+int magot_ctx_elapsed(magot_ctx* ctx, double* ms) {
+  if (int rc = bind(ctx)) return rc;
+  if (!ms) {
+    set_error("magot_ctx_elapsed: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  MAGOT_HIP_TRY(hipEventSynchronize(ctx->mark1));
+  float f = 0.f;
+  MAGOT_HIP_TRY(hipEventElapsedTime(&f, ctx->mark0, ctx->mark1));
+  *ms = f;
+  return MAGOT_OK;
+}
+
+int magot_genome_load_ex(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
+                         uint32_t n_contigs, uint32_t flags, magot_genome** out) {
   if (int rc = bind(ctx)) return rc;
   if (!out || (n_contigs && (!seqs || !lens))) {
     set_error("magot_genome_load: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (flags & ~MAGOT_PACK_HOST) {
+    set_error("magot_genome_load_ex: unknown flags");
     return MAGOT_ERR_ARG;
   }
   *out = nullptr;
@@ -236,22 +278,203 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
     }
   std::vector<ContigSource> src(n_contigs);
   for (uint32_t i = 0; i < n_contigs; ++i) src[i] = ContigSource{seqs[i], lens[i], 0, 0};
-  return load_packed(ctx, src.data(), n_contigs, out);
+  return load_packed(ctx, src.data(), n_contigs, flags, out);
+}
+
+int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t* lens,
+                      uint32_t n_contigs, magot_genome** out) {
+  return magot_genome_load_ex(ctx, seqs, lens, n_contigs, 0u, out);
 }
 
 }  // extern "C"
 
 namespace {
 
-int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, magot_genome** out) {
-  const bool timing = std::getenv("MAGOT_GENOME_TIMING") != nullptr;
-  auto t0 = std::chrono::steady_clock::now();
-  auto lap = [&](const char* what) {
-    if (!timing) return;
+struct Lap {
+  const bool on = std::getenv("MAGOT_GENOME_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  void operator()(const char* what) {
+    if (!on) return;
     const auto t1 = std::chrono::steady_clock::now();
     fprintf(stderr, "[genome] %-8s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
     t0 = t1;
+  }
+};
+
+// Host threads for staging copies: the GPU's share of the host (OMP_NUM_THREADS
+// on the pool's boxes), at most 16.
+unsigned host_threads() {
+  unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) hw = (unsigned)v;
+  }
+  return std::min(hw, 16u);
+}
+
+// Stream the contigs' bytes (FASTA line layout removed) into dev[0, total),
+// total = extent - kOrigin, through two pinned 64 MiB host buffers: host
+// threads fill one while the DMA engine uploads the other.
+int upload_raw(magot_ctx* ctx, const ContigSource* src, const HostPacked& lay, uint8_t* dev) {
+  const uint64_t total = lay.extent - kOrigin;
+  if (!total) return MAGOT_OK;
+  constexpr uint64_t kRing = 64ull << 20;
+  for (int k = 0; k < 2; ++k)
+    if (!ctx->pin[k]) {
+      MAGOT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pin[k]), kRing, hipHostMallocDefault));
+      MAGOT_HIP_TRY(hipEventCreateWithFlags(&ctx->pin_ev[k], hipEventDisableTiming));
+    }
+  const unsigned nt = host_threads();
+  const auto& base = lay.contig_base;
+  auto fill = [&](uint8_t* dst, uint64_t x0, uint64_t x1) {  // raw [x0, x1) -> dst
+    size_t c = std::upper_bound(base.begin(), base.end(), x0 + kOrigin) - base.begin();
+    c = c ? c - 1 : 0;
+    for (; c < base.size() && x0 < x1; ++c) {
+      const uint64_t cb = base[c] - kOrigin, ce = cb + lay.contig_len[c];
+      if (ce <= x0) continue;
+      const uint64_t hi = std::min(ce, x1);
+      copy_bases(src[c], x0 - cb, hi - x0, dst);
+      dst += hi - x0;
+      x0 = hi;
+    }
   };
+  for (uint64_t q0 = 0, k = 0; q0 < total; q0 += kRing, ++k) {
+    const int b = (int)(k & 1);
+    const uint64_t q1 = std::min(total, q0 + kRing);
+    if (k >= 2) MAGOT_HIP_TRY(hipEventSynchronize(ctx->pin_ev[b]));
+    const uint64_t step = ((q1 - q0) + nt - 1) / nt;
+    std::vector<std::thread> pool;
+    for (unsigned i = 1; i < nt && q0 + i * step < q1; ++i) {
+      const uint64_t x0 = q0 + i * step, x1 = std::min(q1, x0 + step);
+      pool.emplace_back([&, x0, x1] { fill(ctx->pin[b] + (x0 - q0), x0, x1); });
+    }
+    fill(ctx->pin[b], q0, std::min(q1, q0 + step));
+    for (auto& t : pool) t.join();
+    MAGOT_HIP_TRY(hipMemcpyAsync(dev + q0, ctx->pin[b], q1 - q0, hipMemcpyHostToDevice,
+                                 ctx->stream));
+    MAGOT_HIP_TRY(hipEventRecord(ctx->pin_ev[b], ctx->stream));
+  }
+  return MAGOT_OK;
+}
+
+// RAII device scratch
+struct DevBuf {
+  void* p = nullptr;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// Device packing: raw bytes streamed to HBM once, runs counted and written by
+// kernels (devpack.hip), the nibble plane packed and mirrored on the device;
+// only the run list (and its directory, built from it) passes through the host.
+int load_device_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs,
+                       magot_genome** out) {
+  Lap lap;
+  HostPacked hp;
+  pack_layout(src, n_contigs, &hp);
+  const uint64_t n = hp.extent - kOrigin;
+  const uint64_t groups = (n + 31) / 32;
+  const size_t scan_bytes = devpack_scan_bytes(groups);
+  Carve sc;
+  const uint64_t o_raw = sc.take<uint8_t>(32 * groups + 64);
+  const uint64_t o_cnt = sc.take<uint32_t>(groups + 1);
+  const uint64_t o_slot = sc.take<uint64_t>(groups + 1);
+  const uint64_t o_tmp = sc.take<uint8_t>(scan_bytes + 1);
+  DevBuf scratch;
+  MAGOT_HIP_TRY(hipMalloc(&scratch.p, sc.used));
+  char* sbase = static_cast<char*>(scratch.p);
+  uint8_t* raw = reinterpret_cast<uint8_t*>(sbase + o_raw);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(sbase + o_cnt);
+  uint64_t* slot = reinterpret_cast<uint64_t*>(sbase + o_slot);
+  // the padding past n is read by the 32-byte loads (and masked)
+  MAGOT_HIP_TRY(hipMemsetAsync(raw + n, 0, 32 * groups + 64 - n, ctx->stream));
+  if (int rc = upload_raw(ctx, src, hp, raw)) return rc;
+  lap("upload");
+  MAGOT_HIP_TRY(launch_run_count(raw, n, cnt, slot, sbase + o_tmp, scan_bytes, ctx->stream));
+  uint64_t n_runs = 0;
+  if (groups) {
+    uint64_t last_slot = 0;
+    uint32_t last_cnt = 0;
+    MAGOT_HIP_TRY(hipMemcpyAsync(&last_slot, slot + groups - 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    MAGOT_HIP_TRY(hipMemcpyAsync(&last_cnt, cnt + groups - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+    n_runs = last_slot + last_cnt;
+  }
+  if (n_runs + 1 >= (uint64_t)kDirClean) {
+    set_error("magot_genome_load: too many exception runs");
+    return MAGOT_ERR_ARG;
+  }
+  DevBuf runs_tmp;
+  std::vector<uint64_t> rs(n_runs), re(n_runs);
+  std::vector<uint8_t> rb(n_runs);
+  if (n_runs) {
+    MAGOT_HIP_TRY(hipMalloc(&runs_tmp.p, n_runs * 17 + 16));
+    uint64_t* d_rs = static_cast<uint64_t*>(runs_tmp.p);
+    uint64_t* d_re = d_rs + n_runs;
+    uint8_t* d_rb = reinterpret_cast<uint8_t*>(d_re + n_runs);
+    launch_run_write(raw, n, slot, d_rs, d_re, d_rb, ctx->stream);
+    MAGOT_HIP_TRY(hipGetLastError());
+    MAGOT_HIP_TRY(hipMemcpyAsync(rs.data(), d_rs, n_runs * 8, hipMemcpyDeviceToHost, ctx->stream));
+    MAGOT_HIP_TRY(hipMemcpyAsync(re.data(), d_re, n_runs * 8, hipMemcpyDeviceToHost, ctx->stream));
+    MAGOT_HIP_TRY(hipMemcpyAsync(rb.data(), d_rb, n_runs, hipMemcpyDeviceToHost, ctx->stream));
+    MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  // ExcRun list: runs longer than the 31-bit length field are split (as the
+  // host packer does), then the sentinel and the directory
+  hp.runs.clear();
+  hp.runs.reserve(n_runs + 1);
+  for (uint64_t k = 0; k < n_runs; ++k) {
+    for (uint64_t a = rs[k]; a < re[k];) {
+      const uint64_t len = std::min<uint64_t>(re[k] - a, 0x7fffffffull);
+      hp.runs.push_back(ExcRun{a, (uint32_t)len, rb[k]});
+      a += len;
+    }
+  }
+  hp.runs.push_back(ExcRun{~0ull, 0, 0});
+  if (hp.runs.size() >= (size_t)kDirClean) {
+    set_error("magot_genome_load: too many exception runs");
+    return MAGOT_ERR_ARG;
+  }
+  exc_runs_directory(&hp);
+  lap("runs");
+  std::unique_ptr<magot_genome> g(new magot_genome());
+  g->ctx = ctx;
+  Carve cv;
+  const uint64_t o_nib = cv.take<uint32_t>(2 * hp.nib_words + 4);
+  const uint64_t o_runs = cv.take<ExcRun>(hp.runs.size());
+  const uint64_t o_dir = cv.take<uint32_t>(hp.dir.size());
+  MAGOT_HIP_TRY(hipMalloc(&g->arena, cv.used));
+  g->arena_bytes = cv.used;
+  char* base = static_cast<char*>(g->arena);
+  g->nib = reinterpret_cast<uint32_t*>(base + o_nib);
+  g->runs = reinterpret_cast<ExcRun*>(base + o_runs);
+  g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
+  launch_nib_pack(raw, n, g->nib, hp.nib_words, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipMemsetAsync(g->nib + 2 * hp.nib_words, 0, 16, ctx->stream));
+  launch_mirror_planes(g->nib, hp.span, ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipMemcpyAsync(g->runs, hp.runs.data(), hp.runs.size() * sizeof(ExcRun),
+                               hipMemcpyHostToDevice, ctx->stream));
+  MAGOT_HIP_TRY(hipMemcpyAsync(g->dir, hp.dir.data(), hp.dir.size() * 4, hipMemcpyHostToDevice,
+                               ctx->stream));
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  g->span = hp.span;
+  g->contig_base = std::move(hp.contig_base);
+  g->contig_len = std::move(hp.contig_len);
+  g->n_runs = hp.runs.size() - 1;
+  g->host_runs = std::move(hp.runs);
+  g->host_dir = std::move(hp.dir);
+  g->extent = hp.extent;
+  g->total_bases = hp.extent - kOrigin;
+  lap("pack");
+  *out = g.release();
+  return MAGOT_OK;
+}
+
+int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, uint32_t flags,
+                magot_genome** out) {
   {
     uint64_t total = 0;
     for (uint32_t i = 0; i < n_contigs; ++i) total += src[i].len;
@@ -263,6 +486,8 @@ int load_packed(magot_ctx* ctx, const ContigSource* src, uint32_t n_contigs, mag
       return MAGOT_ERR_UNSUPPORTED;
     }
   }
+  if (!(flags & MAGOT_PACK_HOST)) return load_device_packed(ctx, src, n_contigs, out);
+  Lap lap;
   HostPacked hp;
   pack_genome(src, n_contigs, &hp);
   lap("pack");
@@ -330,7 +555,7 @@ int magot_genome_load_fasta(magot_ctx* ctx, const char* text, uint64_t len, int 
     fprintf(stderr, "[genome] scan     %.3f s\n",
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
   magot_genome* g = nullptr;
-  if (int rc = load_packed(ctx, fc.src.data(), (uint32_t)fc.src.size(), &g)) return rc;
+  if (int rc = load_packed(ctx, fc.src.data(), (uint32_t)fc.src.size(), 0u, &g)) return rc;
   g->names = std::move(fc.names);
   *out = g;
   return MAGOT_OK;
@@ -439,6 +664,78 @@ int magot_genome_attach(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len, 
   g->runs = reinterpret_cast<ExcRun*>(base + o_runs);
   g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
   *out = g.release();
+  return MAGOT_OK;
+}
+
+int magot_genome_wire_ranges(const magot_genome* g, uint64_t* off, uint64_t* len, uint32_t* n) {
+  if (!g || !off || !len || !n) {
+    set_error("magot_genome_wire_ranges: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  // [forward nibble plane] and [exception runs .. directory end]: the mirror
+  // plane between them (and its 16 bytes of slack) is derived on attach
+  const char* a = static_cast<const char*>(g->arena);
+  off[0] = (uint64_t)((const char*)g->nib - a);
+  len[0] = g->span / 2;  // span bases, 8 per 4-byte word
+  off[1] = (uint64_t)((const char*)g->runs - a);
+  len[1] = g->arena_bytes - off[1];
+  *n = 2;
+  return MAGOT_OK;
+}
+
+int magot_genome_attach_wire(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len,
+                             void* arena_dev, magot_genome** out) {
+  if (int rc = magot_genome_attach(ctx, meta, meta_len, arena_dev, out)) return rc;
+  magot_genome* g = *out;
+  const uint64_t nw = g->span / 8;
+  if ((uint64_t)((char*)g->runs - (char*)g->arena) < (2 * nw + 4) * 4) {
+    magot_genome_destroy(g);
+    *out = nullptr;
+    set_error("magot_genome_attach_wire: malformed genome meta");
+    return MAGOT_ERR_ARG;
+  }
+  hipError_t e = hipMemsetAsync(g->nib + 2 * nw, 0, 16, ctx->stream);
+  if (e == hipSuccess) {
+    launch_mirror_planes(g->nib, g->span, ctx->stream);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) {
+    magot_genome_destroy(g);
+    *out = nullptr;
+    set_error(std::string("magot_genome_attach_wire: ") + hipGetErrorString(e));
+    return MAGOT_ERR_HIP;
+  }
+  return MAGOT_OK;
+}
+
+int magot_copy_segments(magot_ctx* ctx, const void* src_dev, void* dst_dev, const uint64_t* src_off,
+                        const uint64_t* dst_off, uint64_t n) {
+  if (int rc = bind(ctx)) return rc;
+  if (!src_off || !dst_off) {
+    set_error("magot_copy_segments: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (!n || dst_off[n] == dst_off[0]) return MAGOT_OK;
+  if (!src_dev || !dst_dev) {
+    set_error("magot_copy_segments: null buffer");
+    return MAGOT_ERR_ARG;
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (dst_off[i + 1] < dst_off[i]) {
+      set_error("magot_copy_segments: dst_off must be non-decreasing");
+      return MAGOT_ERR_ARG;
+    }
+  DevBuf tables;
+  MAGOT_HIP_TRY(hipMalloc(&tables.p, (2 * n + 1) * 8));
+  uint64_t* d_src = static_cast<uint64_t*>(tables.p);
+  uint64_t* d_dst = d_src + n;
+  MAGOT_HIP_TRY(hipMemcpyAsync(d_src, src_off, n * 8, hipMemcpyHostToDevice, ctx->stream));
+  MAGOT_HIP_TRY(hipMemcpyAsync(d_dst, dst_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream));
+  launch_segments_copy(static_cast<const uint8_t*>(src_dev), d_src, d_dst, n,
+                       static_cast<uint8_t*>(dst_dev), ctx->stream);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   return MAGOT_OK;
 }
 
@@ -1034,12 +1331,17 @@ int magot_translate(magot_ctx* ctx, const uint8_t* seq, uint64_t len, int frame,
     return MAGOT_ERR_ARG;
   }
   const uint8_t st = (uint8_t)strand;
-  if (int rc = magot_translate_batch(ctx, seq, off, 1, &fr, &st, nullptr, poff, out)) return rc;
+  // translated into a private buffer, so exactly *out_len bytes reach `out`
+  std::vector<uint8_t> tmp((size_t)codons + 1);
+  if (int rc = magot_translate_batch(ctx, seq, off, 1, &fr, &st, nullptr, poff, tmp.data()))
+    return rc;
   int64_t n = codons;
-  if (trimX && n > 0 && out[0] == 'X') {  // genome.py:819-821
-    std::memmove(out, out + 1, (size_t)(n - 1));
+  const uint8_t* res = tmp.data();
+  if (trimX && n > 0 && res[0] == 'X') {  // genome.py:819-821
+    ++res;
     --n;
   }
+  if (n) std::memcpy(out, res, (size_t)n);
   *out_len = n;
   return MAGOT_OK;
 }
@@ -1238,6 +1540,12 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
         for (uint64_t e = ie[r]; e < ie[r + 1]; ++e) {
           const uint64_t st = starts[e];
           if (starts[e + 1] == st || st >= noff[r + 1]) continue;  // empty
+          // the remap assumes no compacted interval crosses a record end
+          // (compaction only drops empty intervals, magot_plan_create)
+          if (starts[e + 1] > noff[r + 1]) {
+            set_error("magot_plan_orf6: an interval crosses the end of its record");
+            return MAGOT_ERR_STATE;
+          }
           const uint64_t st_k = noff_k[k] + (st - noff[r]);
           rows_k[2 * j] = rows[2 * e] + st - st_k;  // the same unified anchor
           rows_k[2 * j + 1] = st_k | (rows[2 * e + 1] & kOrf6ExcRow);
@@ -1352,6 +1660,18 @@ int magot_orf6_fetch(magot_ctx* ctx, magot_orf6* o, uint8_t* out, uint64_t* stre
     std::vector<uint64_t> tmp(6 * o->n_rec + 1);
     return magot_orf6_sizes(o->plan->nuc_off.data(), o->n_rec, tmp.data(), stream_len, nullptr);
   }
+  return MAGOT_OK;
+}
+
+int magot_orf6_copy_outputs(magot_ctx* ctx, magot_orf6* o, void* dst_dev) {
+  if (int rc = bind(ctx)) return rc;
+  if (!o || !dst_dev) {
+    set_error("magot_orf6_copy_outputs: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (o->total)
+    MAGOT_HIP_TRY(hipMemcpyAsync(dst_dev, o->out, o->total, hipMemcpyDeviceToDevice, ctx->stream));
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   return MAGOT_OK;
 }
 

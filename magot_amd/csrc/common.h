@@ -74,6 +74,30 @@ void copy_contig(const ContigSource& src, uint8_t* dst);
 
 // Packs contig bytes (multi-threaded host code, pack.cpp).
 void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out);
+// The coordinate layout alone (contig bases, extent, span, nib_words).
+void pack_layout(const ContigSource* src, uint32_t n, HostPacked* out);
+// out->dir from out->runs (sorted, sentinel appended) and out->extent.
+void exc_runs_directory(HostPacked* out);
+// bases [pos, pos + n) of a contig, contiguous, into dst (fasta.cpp).
+void copy_bases(const ContigSource& src, uint64_t pos, uint64_t n, uint8_t* dst);
+
+// Device packing (devpack.hip): raw = the contigs' bytes concatenated in
+// coordinate order (raw index i = global base kOrigin + i), n bytes, padded
+// with readable bytes to a multiple of 32.
+size_t devpack_scan_bytes(uint64_t n_groups);
+// count[g] = exception runs starting in raw bytes [32g, 32g+32); slot = their
+// exclusive prefix sum (n_groups = ceil(n / 32) entries each).
+hipError_t launch_run_count(const uint8_t* raw, uint64_t n, uint32_t* count, uint64_t* slot,
+                            void* scan_tmp, size_t scan_bytes, hipStream_t s);
+// every run's first coordinate, end coordinate (exclusive) and byte, in order
+void launch_run_write(const uint8_t* raw, uint64_t n, const uint64_t* slot, uint64_t* run_start,
+                      uint64_t* run_end, uint8_t* run_byte, hipStream_t s);
+// the forward nibble plane, nib_words words (pad bases 0)
+void launch_nib_pack(const uint8_t* raw, uint64_t n, uint32_t* nib, uint64_t nib_words,
+                     hipStream_t s);
+// dst[dst_off[i], dst_off[i+1]) = src[src_off[i], ...) for i < n (devpack.hip)
+void launch_segments_copy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off,
+                          uint64_t n, uint8_t* dst, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Extraction tiling
@@ -87,10 +111,9 @@ constexpr int kChunk = 16;                    // bytes per lane-store
 // share -2.7 %; but the 2-GPU share +8 %, C2 (nucleotides only) +5.5 %, and at
 // full C3 size 4 slots are +3.6 % slower; A/Bs in DESIGN.md).
 constexpr int kLaneChunksLarge = 5, kLaneChunksSmall = 3;
-constexpr int kLaneChunks = kLaneChunksLarge;   // the larger tile (LDS sizing, clamps)
-constexpr int kSlots = 64 * kLaneChunks;        // 320 chunk slots per wave tile
-constexpr int kTile = (kSlots - 3) * kChunk;    // 5072 output bytes per tile (3 slots of halo):
-                                                // <= 1691 residues, <= 106 residue chunks
+// Output bytes of a tile cut for `lane_chunks` slots per lane (3 slots of halo):
+// 5072 for the large tile (<= 1691 residues, <= 106 residue chunks), 3024 for
+// the small one.  Size any per-tile storage with the template's LC.
 constexpr int tile_bytes(int lane_chunks) { return (64 * lane_chunks - 3) * 16; }
 // plans whose large-tile count is below this use the small tile
 constexpr uint64_t kSmallTilePlan = 40000;
@@ -129,16 +152,12 @@ constexpr uint32_t kLitHi = 0x4E4D4B59u;  // classes 4..7: Y K M (7: never writt
 // One 16-byte output store with the non-temporal hint (global_store_dwordx4
 // ... nt): the outputs are written once and never re-read by the kernel, so
 // they stream through L2 instead of displacing genome lines.  A/B on one box
-// (200 back-to-back C3 steps): 0.2905 -> 0.2779 ms per step.  Build with
-// -DMAGOT_EXP_PLAIN_STORE for the plain store (A/B only).
+// (200 back-to-back C3 steps): 0.2905 -> 0.2779 ms per step (the plain-store
+// variant: scripts/experiments/plain_store.patch).
 __device__ __forceinline__ void store16(uint8_t* dst, uint4 v) {
-#ifdef MAGOT_EXP_PLAIN_STORE
-  *reinterpret_cast<uint4*>(dst) = v;
-#else
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   u32x4 x = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst));
-#endif
 }
 
 // Debug switches carried in ExtractArgs.outputs (env MAGOT_DEBUG_PATHS):
@@ -148,7 +167,7 @@ constexpr uint32_t kDebugSlowPep = 1u << 9;
 
 // Device plan.  Zero-length intervals and records without a codon are
 // compacted away on the host (they add no output); tiles are 16-byte aligned
-// ranges of the nucleotide output of at most kTile bytes, cut shorter where
+// ranges of the nucleotide output of at most tile_bytes(lane_chunks) bytes, cut shorter where
 // they would touch more than kExonCap intervals or kTxCap records.
 struct ExtractArgs {
   // Nibble plane in unified coordinates: [0, span) forward strand, [span,

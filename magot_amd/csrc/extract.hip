@@ -12,9 +12,11 @@
 //
 // Work decomposition (output-stationary, HBM-bound):
 //   * The host cuts the concatenated nucleotide output into 16-byte aligned
-//     tiles of <= kTile = 5072 bytes (317 chunks of 16 bytes; shorter where a
+//     tiles of <= tile_bytes(LC) bytes, LC = the chunk slots per lane the plan
+//     was cut for (5: 5072 bytes = 317 chunks of 16 for large plans; 3: 3024
+//     bytes for translating plans under kSmallTilePlan tiles; shorter where a
 //     tile would touch more than kExonCap intervals or kTxCap records).  A
-//     tile belongs to ONE wavefront: 64 lanes x 5 chunk slots (317 output
+//     tile belongs to ONE wavefront: 64 lanes x LC chunk slots (the tile's
 //     chunks + a 3-chunk halo for codons that run past the tile end) and 1-2
 //     residue chunks per lane, so there is no workgroup barrier (every wave
 //     writes its own copy of the codon table).

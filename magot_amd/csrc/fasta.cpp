@@ -211,6 +211,24 @@ int scan_fasta(const char* text, uint64_t n, bool truncate, FastaContigs* out) {
   return MAGOT_OK;
 }
 
+void copy_bases(const ContigSource& src, uint64_t pos, uint64_t n, uint8_t* dst) {
+  if (!n) return;
+  if (!src.width) {
+    memcpy(dst, src.ptr + pos, n);
+    return;
+  }
+  uint64_t line = pos / src.width, off = pos - line * src.width;
+  const uint8_t* p = src.ptr + line * (src.width + src.term) + off;
+  while (n) {
+    const uint64_t k = std::min(n, src.width - off);
+    memcpy(dst, p, k);
+    dst += k;
+    n -= k;
+    p += k + src.term;
+    off = 0;
+  }
+}
+
 void copy_contig(const ContigSource& src, uint8_t* dst) {
   if (!src.width) {
     if (src.len) memcpy(dst, src.ptr, src.len);

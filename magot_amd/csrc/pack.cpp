@@ -126,7 +126,7 @@ void pack_piece(const ContigSource* src, const HostPacked& layout, uint64_t p0, 
 
 }  // namespace
 
-void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out) {
+void pack_layout(const ContigSource* src, uint32_t n, HostPacked* out) {
   out->contig_base.resize(n);
   out->contig_len.resize(n);
   uint64_t cur = kOrigin;
@@ -139,6 +139,25 @@ void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out) {
   const uint64_t padded = cur + 64;
   out->span = (padded + 64 + 31) & ~31ull;
   out->nib_words = out->span / 8;
+}
+
+void exc_runs_directory(HostPacked* out) {
+  // Directory: first run whose end lies past the block start.
+  const uint64_t padded = out->extent + 64;
+  const uint64_t nblocks = ((padded + 4095) >> kDirShift) + 2;
+  out->dir.assign(nblocks, 0);
+  size_t r = 0, nr = out->runs.size() - 1;
+  for (uint64_t b = 0; b < nblocks; ++b) {
+    uint64_t bs = b << kDirShift, be = bs + (1ull << kDirShift);
+    while (r < nr && out->runs[r].start + out->runs[r].len <= bs) ++r;
+    uint32_t v = (uint32_t)r;
+    if (out->runs[r].start >= be) v |= kDirClean;
+    out->dir[b] = v;
+  }
+}
+
+void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out) {
+  pack_layout(src, n, out);
   out->nib.reset(new uint32_t[out->nib_words]);  // written in full by the pieces
 
   // Split [0, span) into 32-aligned pieces for the worker threads.
@@ -179,18 +198,7 @@ void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out) {
     }
   }
   out->runs.push_back(ExcRun{~0ull, 0, 0});  // sentinel
-
-  // Directory: first run whose end lies past the block start.
-  const uint64_t nblocks = ((padded + 4095) >> kDirShift) + 2;
-  out->dir.assign(nblocks, 0);
-  size_t r = 0, nr = out->runs.size() - 1;
-  for (uint64_t b = 0; b < nblocks; ++b) {
-    uint64_t bs = b << kDirShift, be = bs + (1ull << kDirShift);
-    while (r < nr && out->runs[r].start + out->runs[r].len <= bs) ++r;
-    uint32_t v = (uint32_t)r;
-    if (out->runs[r].start >= be) v |= kDirClean;
-    out->dir[b] = v;
-  }
+  exc_runs_directory(out);
 }
 
 }  // namespace magot

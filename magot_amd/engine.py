@@ -38,7 +38,11 @@ class DeviceGenome(object):
     (latin-1, one char per byte) or ``bytes``.
     """
 
-    def __init__(self, contigs, ctx=None):
+    def __init__(self, contigs, ctx=None, pack='device'):
+        """``pack``: 'device' (default: raw bytes streamed to HBM once, packed
+        by kernels) or 'host' (pack.cpp, then the plane uploaded)."""
+        if pack not in ('device', 'host'):
+            raise ValueError(pack)
         self.ctx = ctx or _lib.default_context()
         names = []
         bufs = []
@@ -56,8 +60,9 @@ class DeviceGenome(object):
         lens = np.ascontiguousarray(self.lengths)
         h = ctypes.c_void_p()
         L = _lib.lib()
-        check(L.magot_genome_load(self.ctx.handle, ptrs, lens.ctypes.data_as(_lib._u64p), n,
-                                  ctypes.byref(h)), 'magot_genome_load')
+        flags = _lib.PACK_HOST if pack == 'host' else 0
+        check(L.magot_genome_load_ex(self.ctx.handle, ptrs, lens.ctypes.data_as(_lib._u64p), n,
+                                     flags, ctypes.byref(h)), 'magot_genome_load')
         self.handle = h
         self._keepalive = None
         self._stats()
@@ -82,15 +87,28 @@ class DeviceGenome(object):
                                     ctypes.byref(ab)), 'magot_genome_export')
         return meta.tobytes(), ab.value
 
+    def wire_ranges(self):
+        """[(offset, length)] of the arena a replica must receive (the forward
+        plane, then runs + directory); the mirror is rebuilt on attach."""
+        off = np.zeros(2, dtype=np.uint64)
+        ln = np.zeros(2, dtype=np.uint64)
+        n = ctypes.c_uint32()
+        check(_lib.lib().magot_genome_wire_ranges(self.handle, off.ctypes.data_as(_lib._u64p),
+                                                  ln.ctypes.data_as(_lib._u64p), ctypes.byref(n)),
+              'magot_genome_wire_ranges')
+        return [(int(off[k]), int(ln[k])) for k in range(n.value)]
+
     def copy_arena(self, dst_dev_ptr):
         """D2D copy of the packed arena to caller device memory (an address)."""
         check(_lib.lib().magot_genome_copy_arena(self.handle, ctypes.c_void_p(dst_dev_ptr)),
               'magot_genome_copy_arena')
 
     @classmethod
-    def attach(cls, meta, arena_dev_ptr, names, lengths, ctx=None, keepalive=None):
+    def attach(cls, meta, arena_dev_ptr, names, lengths, ctx=None, keepalive=None, wire=False):
         """A genome over caller device memory that holds a broadcast arena.
-        ``keepalive`` (e.g. the tensor owning the memory) lives as long as this."""
+        ``keepalive`` (e.g. the tensor owning the memory) lives as long as this.
+        ``wire=True``: the memory holds only the wire ranges; the mirror plane
+        is rebuilt on this device (magot_genome_attach_wire)."""
         self = cls.__new__(cls)
         self.ctx = ctx or _lib.default_context()
         self.names = list(names)
@@ -99,8 +117,8 @@ class DeviceGenome(object):
         self._keepalive = keepalive
         m = np.frombuffer(meta, dtype=np.uint8)
         h = ctypes.c_void_p()
-        check(_lib.lib().magot_genome_attach(self.ctx.handle, ptr(m), len(m),
-                                             ctypes.c_void_p(arena_dev_ptr), ctypes.byref(h)),
+        fn = _lib.lib().magot_genome_attach_wire if wire else _lib.lib().magot_genome_attach
+        check(fn(self.ctx.handle, ptr(m), len(m), ctypes.c_void_p(arena_dev_ptr), ctypes.byref(h)),
               'magot_genome_attach')
         self.handle = h
         self._stats()
@@ -634,6 +652,13 @@ class Orf6Plan(object):
                                           ptr(soff), ptr(slen)), 'magot_orf6_fetch')
         return soff, slen[:6 * self.plan.n_tx]
 
+    def copy_outputs(self, dst_dev_ptr):
+        """D2D copy of the padded residue bytes (``total``) into caller device
+        memory (an address), e.g. the buffer an output gather sends."""
+        check(_lib.lib().magot_orf6_copy_outputs(self.ctx.handle, self.handle,
+                                                 ctypes.c_void_p(dst_dev_ptr)),
+              'magot_orf6_copy_outputs')
+
     def time(self, iters):
         ms = ctypes.c_double()
         check(_lib.lib().magot_orf6_time(self.ctx.handle, self.handle, int(iters),
@@ -656,6 +681,30 @@ class Orf6Plan(object):
             self.close()
         except Exception:
             pass
+
+
+def copy_segments(src_dev_ptr, dst_dev_ptr, src_off, dst_off, ctx=None):
+    """dst[dst_off[i]:dst_off[i+1]] = src[src_off[i]:...] on the device
+    (magot_copy_segments; addresses of device memory, host offset tables)."""
+    ctx = ctx or _lib.default_context()
+    so = np.ascontiguousarray(src_off, dtype=np.uint64)
+    do = np.ascontiguousarray(dst_off, dtype=np.uint64)
+    if len(do) != len(so) + 1:
+        raise ValueError('dst_off needs len(src_off) + 1 entries')
+    check(_lib.lib().magot_copy_segments(ctx.handle, ctypes.c_void_p(src_dev_ptr),
+                                         ctypes.c_void_p(dst_dev_ptr), ptr(so), ptr(do), len(so)),
+          'magot_copy_segments')
+
+
+def orf6_sizes(rec_off):
+    """(stream_off 6n+1, stream_len 6n) of the six-frame layout over records
+    with nucleotide offsets ``rec_off`` (n+1): magot_orf6_sizes."""
+    off = np.ascontiguousarray(rec_off, dtype=np.uint64)
+    n = len(off) - 1
+    soff = np.empty(6 * n + 1, dtype=np.uint64)
+    slen = np.empty(max(6 * n, 1), dtype=np.uint64)
+    check(_lib.lib().magot_orf6_sizes(ptr(off), n, ptr(soff), ptr(slen), None), 'magot_orf6_sizes')
+    return soff, slen[:6 * n]
 
 
 def codon_symbols(seq, class256, n_classes, lut, ctx=None):
@@ -708,4 +757,5 @@ def translate_batch(seqs, frames, strands, lut64=None, ctx=None):
 __all__ = ['DeviceGenome', 'ExtractionPlan', 'revcomp_batch', 'translate_batch', 'codon_symbols',
            'OUT_NUC',
            'OUT_PEP', 'MagotError', 'GffPlan', 'orf6_batch', 'Orf6Plan', 'fasta_read',
-           'FastaGenome', 'PartitionedGenome', 'device_genome', 'extract_records', 'plan_parts']
+           'FastaGenome', 'PartitionedGenome', 'device_genome', 'extract_records', 'plan_parts',
+           'copy_segments', 'orf6_sizes']

@@ -176,6 +176,73 @@ def _lookup(library, triplet):
         return 'X'
 
 
+def _same_items(a, b):
+    """Two snapshots of a library's items, values compared as the symbol
+    table distinguishes them (identity, or same type and equal)."""
+    return len(a) == len(b) and all(
+        ka == kb and (va is vb or (type(va) is type(vb) and va == vb))
+        for (ka, va), (kb, vb) in zip(a, b))
+
+
+_LIBRARY_TABLES = []  # [(id, items snapshot, tables)], most recent last
+
+
+def _library_tables(library):
+    """(chars, class256, K, values, symbol lut) of a codon library for
+    magot_codon_symbols: the extended alphabet (ACGT, the other characters of
+    matchable 3-character keys, 'other'), the byte -> class map, and for every
+    class triplet the index of its value in ``values`` (one entry per distinct
+    value).  Cached per library object while its items are unchanged, so
+    get_orfs' six translate() calls build it once."""
+    items = list(library.items())
+    for i, (lid, snap, tables) in enumerate(_LIBRARY_TABLES):
+        if lid == id(library) and _same_items(snap, items):
+            _LIBRARY_TABLES.append(_LIBRARY_TABLES.pop(i))
+            return tables
+    chars = list(_ACGT)
+    for key in library.keys():
+        if _matchable(key) and len(key) == 3:
+            for c in key:
+                if c not in chars:
+                    chars.append(c)
+    K = len(chars) + 1
+    if K ** 3 > 32768:
+        raise NotImplementedError('codon library keys use more than 31 distinct characters')
+    cls = np.full(256, K - 1, dtype=np.uint8)
+    for i, c in enumerate(chars):
+        if ord(c) < 256:
+            cls[ord(c)] = i
+    for b in range(ord('a'), ord('z') + 1):
+        cls[b] = cls[b - 32]
+    values, lut = [], np.zeros(K ** 3, dtype=np.uint8)
+    seen = {}  # (type, value) -> index, for hashable values
+    for x in range(K ** 3):
+        c0, c1, c2 = x % K, (x // K) % K, x // (K * K)
+        if K - 1 in (c0, c1, c2):
+            v = 'X'                                    # no key holds this character
+        else:
+            v = _lookup(library, chars[c0] + chars[c1] + chars[c2])
+        try:
+            key = (type(v), v)
+            j = seen.get(key)
+        except TypeError:                              # unhashable value: linear scan
+            key = None
+            j = next((i for i, u in enumerate(values)
+                      if u is v or (type(u) is type(v) and u == v)), None)
+        if j is None:
+            if len(values) == 256:
+                raise NotImplementedError('codon library has more than 256 distinct values')
+            values.append(v)
+            j = len(values) - 1
+            if key is not None:
+                seen[key] = j
+        lut[x] = j
+    tables = (chars, cls, K, values, lut)
+    _LIBRARY_TABLES.append((id(library), items, tables))
+    del _LIBRARY_TABLES[:-8]
+    return tables
+
+
 def _translate_general(s, library, frame, strand, trimX):
     """Sequence.translate (genome.py:795-822) for any library and any integer
     frame.  The characters the loop visits -- positions frame .. len-1, a
@@ -200,38 +267,7 @@ def _translate_general(s, library, frame, strand, trimX):
     first = _lookup(library, _ascii_upper(V[:J]))
     body = V[J:]
     m = len(body) // 3
-    # extended alphabet: ACGT, the other characters of matchable 3-char keys, other
-    chars = list(_ACGT)
-    for key in library.keys():
-        if _matchable(key) and len(key) == 3:
-            for c in key:
-                if c not in chars:
-                    chars.append(c)
-    K = len(chars) + 1
-    if K ** 3 > 32768:
-        raise NotImplementedError('codon library keys use more than 31 distinct characters')
-    cls = np.full(256, K - 1, dtype=np.uint8)
-    for i, c in enumerate(chars):
-        if ord(c) < 256:
-            cls[ord(c)] = i
-    for b in range(ord('a'), ord('z') + 1):
-        cls[b] = cls[b - 32]
-    values, lut = [], np.zeros(K ** 3, dtype=np.uint8)
-    for x in range(K ** 3):
-        c0, c1, c2 = x % K, (x // K) % K, x // (K * K)
-        if K - 1 in (c0, c1, c2):
-            v = 'X'                                    # no key holds this character
-        else:
-            v = _lookup(library, chars[c0] + chars[c1] + chars[c2])
-        for j, u in enumerate(values):
-            if u is v or (type(u) is type(v) and u == v):
-                break
-        else:
-            if len(values) == 256:
-                raise NotImplementedError('codon library has more than 256 distinct values')
-            values.append(v)
-            j = len(values) - 1
-        lut[x] = j
+    chars, cls, K, values, lut = _library_tables(library)
     sym = engine.codon_symbols(V[J:J + 3 * m], cls, K, lut)
     if not isinstance(first, str):
         raise TypeError('can only concatenate str (not "%s") to str' % type(first).__name__)

@@ -7,8 +7,6 @@
     python -m magot_amd.genome_tools extract_upstream_downstream <fasta> <gff> <length> up|down
            [feature_type=gene] [namefrom=ID] [truncate_names=True]
     python -m magot_amd.genome_tools coords2fasta <fasta> <seqid> <start> <stop> [truncate_names=False]
-    python -m magot_amd.genome_tools dna2orfs <fasta> <output_file>   (broken in the reference:
-           TypeError, reproduced)
     python -m magot_amd.genome_tools blast_csv2fasta <fasta> <blast.csv> [order=py2|insertion]
     python -m magot_amd.genome_tools exonerate2fasta <fasta> <exonerate.txt> [order=py2|insertion]
     python -m magot_amd.genome_tools get_seq_from_fasta <fasta> <seq_name> [truncate_names=False]
@@ -344,35 +342,9 @@ def get_seq_from_fasta(genome_sequence, seq_name, truncate_names='False'):
     _write(g.get_scaffold_fasta(seq_name) + '\n')
 
 
-def dna2orfs(fasta_location, output_file, from_atg=False, longest=False):
-    """genome_tools.py:145-180.  The reference builds a Genome, opens
-    output_file for writing and then calls ``.translate(frame=, strand=)`` on
-    each contig's plain ``str`` (GenomeSequence values are str,
-    genome.py:870-877): that is ``str.translate``, which takes no keyword
-    arguments, so with at least one contig it raises TypeError and leaves the
-    output file empty -- on Python 2.7 as here (tests/golden/orfs.json, from
-    the reference).  Reproduced as is; the working six-frame path is
-    ``Sequence.get_orfs`` (orf6_kernel)."""
-    dna = genome.Genome(fasta_location)
-    with open(output_file, 'w'):
-        for _ in dna.genome_sequence:
-            raise TypeError('translate() takes no keyword arguments')
-
-
-def get_CDS_peptides(genome_sequence, gff, output_location, gene_name_filters=[],
-                     gene_length_filter=None, names_from='CDS'):
-    """genome_tools.py:283-322.  The reference reads the genome, then calls
-    ``Genome.read_gff3``, which genome.py never defines: AttributeError
-    before the output file is opened (Python 2.7 and 3 alike).  Reproduced
-    as is; its intent, the longest ORF per CDS, is Sequence.get_orfs
-    (orf6_kernel) on each CDS's get_seq()."""
-    genome.Genome(genome_sequence)
-    raise AttributeError("Genome instance has no attribute 'read_gff3'")
-
-
-TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep, 'get_CDS_peptides': get_CDS_peptides,
+TOOLS = {'gff2fasta': gff2fasta, 'cds2pep': cds2pep,
          'extract_upstream_downstream': extract_upstream_downstream,
-         'coords2fasta': coords2fasta, 'dna2orfs': dna2orfs,
+         'coords2fasta': coords2fasta,
          'blast_csv2fasta': blast_csv2fasta, 'exonerate2fasta': exonerate2fasta,
          'get_seq_from_fasta': get_seq_from_fasta}
 

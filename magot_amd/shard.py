@@ -3,9 +3,10 @@
 One process per GPU (torchrun); ``torch.distributed`` with the nccl backend is
 RCCL over xGMI on MI355X.  The job:
 
-  1. rank 0 packs the genome once (magot_genome_load) and the packed arena is
-     broadcast device-to-device to every rank (``replicate_genome``); the
-     other ranks attach to the received bytes (magot_genome_attach);
+  1. rank 0 packs the genome once (magot_genome_load) and the packed arena's
+     wire ranges (forward plane, runs, directory) are broadcast device-to-
+     device to every rank (``replicate_genome``); the other ranks attach to
+     the received bytes and rebuild the mirror plane (magot_genome_attach_wire);
   2. records are sharded in genome order into equal-weight ranges
      (``record_shards``: contigs stay whole except where a range boundary
      splits one at a transcript boundary), so a record never spans ranks and
@@ -14,7 +15,8 @@ RCCL over xGMI on MI355X.  The job:
   4. outputs go back per rank by D2H into pinned host memory (the host is
      the consumer), or are gathered to rank 0 over the collective backend
      (``Gather``: a size exchange, then one padded gather of each output
-     buffer); ``reassemble`` restores global record order.
+     buffer into a rank-major buffer); ``reassemble_device`` restores global
+     record order with one segment-copy kernel (magot_copy_segments).
 
 With the gloo backend (CPU tests) the same steps run with host tensors.
 """
@@ -92,8 +94,12 @@ def _device(dist):
 def replicate_genome(dist, rank, contigs, ctx):
     """The packed genome on every rank: packed once on rank 0, broadcast.
 
+    Only the arena's wire ranges cross the links (the forward nibble plane,
+    the exception runs and their directory: magot_genome_wire_ranges); every
+    receiving rank rebuilds the reverse-strand mirror on its own device
+    (magot_genome_attach_wire), so the broadcast moves half the arena.
     ``contigs`` is the (name, sequence) list on rank 0 (ignored elsewhere).
-    Returns (DeviceGenome, seconds spent in the broadcast)."""
+    Returns (DeviceGenome, seconds spent in the broadcast, bytes broadcast)."""
     import time
 
     import torch
@@ -102,12 +108,12 @@ def replicate_genome(dist, rank, contigs, ctx):
     if rank == 0:
         dev = engine.DeviceGenome(contigs, ctx=ctx)
         meta, nbytes = dev.export()
-        info = [meta, nbytes, dev.names, [int(x) for x in dev.lengths]]
+        info = [meta, nbytes, dev.names, [int(x) for x in dev.lengths], dev.wire_ranges()]
     else:
         dev = None
-        info = [None, None, None, None]
+        info = [None, None, None, None, None]
     dist.broadcast_object_list(info, src=0)
-    meta, nbytes, names, lengths = info
+    meta, nbytes, names, lengths, ranges = info
     where = _device(dist)
     buf = torch.empty(nbytes, dtype=torch.uint8, device='cuda')
     if rank == 0:
@@ -115,26 +121,30 @@ def replicate_genome(dist, rank, contigs, ctx):
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    if where == 'cuda':
-        dist.broadcast(buf, src=0)
-    else:
-        host = buf.cpu()
-        dist.broadcast(host, src=0)
-        buf.copy_(host)
+    for off, ln in ranges:
+        part = buf[off:off + ln]
+        if where == 'cuda':
+            dist.broadcast(part, src=0)
+        else:
+            host = part.cpu()
+            dist.broadcast(host, src=0)
+            part.copy_(host)
     torch.cuda.synchronize()
     t_bcast = time.perf_counter() - t0
     if rank != 0:
         dev = engine.DeviceGenome.attach(meta, buf.data_ptr(), names, lengths, ctx=ctx,
-                                         keepalive=buf)
-    return dev, t_bcast
+                                         keepalive=buf, wire=True)
+    return dev, t_bcast, sum(ln for _, ln in ranges)
 
 
 class Gather(object):
     """Variable-size byte buffers from every rank to rank 0, buffers allocated
     once: ``send`` (capacity = the largest rank's size) is filled by the
     caller (e.g. magot_plan_copy_outputs), ``run()`` gathers it on the
-    collective backend (device to device with nccl/RCCL), ``parts()`` gives
-    rank 0 the per-rank bytes as numpy arrays."""
+    collective backend (device to device with nccl/RCCL) into one rank-major
+    receive buffer on rank 0 (rank r's bytes at r * ``cap``): ``parts()`` as
+    numpy arrays, ``received()`` the whole buffer on the device (for
+    ``reassemble_device``)."""
 
     def __init__(self, dist, rank, world, nbytes, device='cuda'):
         import torch
@@ -145,12 +155,16 @@ class Gather(object):
         all_sizes = [torch.zeros(1, dtype=torch.int64, device=where) for _ in range(world)]
         dist.all_gather(all_sizes, sizes)
         self.sizes = [int(x.item()) for x in all_sizes]
-        cap = max(max(self.sizes), 1)
+        # 16-byte aligned slots, so aligned records stay aligned in the buffer
+        self.cap = cap = (max(max(self.sizes), 1) + 15) & ~15
+        self.device = device
         self.send = torch.zeros(cap, dtype=torch.uint8, device=device)
         self._host = torch.empty(cap, dtype=torch.uint8) if self.staged else None
         buf_dev = 'cpu' if self.staged else device
-        self.recv = [torch.empty(cap, dtype=torch.uint8, device=buf_dev)
-                     for _ in range(world)] if rank == 0 else None
+        self.recv_all = torch.empty(world * cap, dtype=torch.uint8, device=buf_dev) \
+            if rank == 0 else None
+        self.recv = [self.recv_all[r * cap:(r + 1) * cap] for r in range(world)] \
+            if rank == 0 else None
 
     def run(self):
         src = self.send
@@ -164,6 +178,12 @@ class Gather(object):
             return None
         return [self.recv[r][:self.sizes[r]].cpu().numpy() for r in range(self.world)]
 
+    def received(self):
+        """Rank 0: the rank-major receive buffer as a device tensor."""
+        if self.rank != 0:
+            return None
+        return self.recv_all if not self.staged else self.recv_all.to(self.device)
+
 
 def gather_bytes(dist, rank, world, src_tensor, nbytes):
     """One-off gather of ``nbytes`` of ``src_tensor`` from every rank to rank 0
@@ -175,18 +195,73 @@ def gather_bytes(dist, rank, world, src_tensor, nbytes):
     return g.parts()
 
 
-def reassemble(shards, parts, offs):
-    """Global-order bytes + offsets from per-rank (bytes, offsets) in shard order."""
-    n_rec = sum(len(s) for s in shards)
+def gather_offsets(dist, rank, world, off):
+    """Every rank's offset table (uint64, its records + 1) to rank 0, over the
+    collective backend (one padded gather, no pickling): a list of numpy
+    arrays on rank 0, None elsewhere."""
+    import torch
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    where = _device(dist)
+    n = torch.tensor([len(off)], dtype=torch.int64, device=where)
+    ns = [torch.zeros(1, dtype=torch.int64, device=where) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    cap = max(ns)
+    send = torch.zeros(cap, dtype=torch.int64, device=where)
+    send[:len(off)] = torch.from_numpy(off).to(where)
+    recv = [torch.zeros(cap, dtype=torch.int64, device=where) for _ in range(world)] \
+        if rank == 0 else None
+    dist.gather(send, gather_list=recv, dst=0)
+    if rank != 0:
+        return None
+    return [recv[r][:ns[r]].cpu().numpy() for r in range(world)]
+
+
+def reassembly_tables(shards, offs, cap):
+    """Segment tables that put per-rank outputs back into global record order.
+
+    ``shards[r]``: rank r's global record ids in its output order; ``offs[r]``:
+    its output offsets (records + 1 entries: record j is bytes [offs[r][j],
+    offs[r][j+1]) of its part); ``cap``: the rank stride of the gathered
+    buffer.  Returns (src_off, dst_off, goff) for magot_copy_segments, with
+    goff the global offsets (n+1): dst is laid out in global record order."""
+    n_rec = sum(len(sh) for sh in shards)
     lens = np.zeros(n_rec, dtype=np.int64)
-    for sh, off in zip(shards, offs):
+    src_off = np.zeros(n_rec, dtype=np.uint64)
+    for r, (sh, off) in enumerate(zip(shards, offs)):
         off = np.asarray(off, dtype=np.int64)
+        sh = np.asarray(sh, dtype=np.int64)
+        if len(off) != len(sh) + 1:
+            raise ValueError('rank %d: %d offsets for %d records' % (r, len(off), len(sh)))
         lens[sh] = off[1:] - off[:-1]
+        src_off[sh] = (r * int(cap) + off[:-1]).astype(np.uint64)
     goff = np.zeros(n_rec + 1, dtype=np.int64)
     np.cumsum(lens, out=goff[1:])
-    out = np.empty(int(goff[-1]), dtype=np.uint8)
-    for sh, part, off in zip(shards, parts, offs):
-        off = np.asarray(off, dtype=np.int64)
-        for j, rec in enumerate(sh):
-            out[goff[rec]:goff[rec + 1]] = part[off[j]:off[j + 1]]
-    return out, goff
+    return src_off, goff.astype(np.uint64), goff
+
+
+def reassemble_device(shards, offs, gathered, cap, ctx=None):
+    """Global-order output on the device from a rank-major gathered buffer
+    (``gathered``: a device tensor, rank r's part at r * cap): one
+    magot_copy_segments launch.  Returns (device tensor, global offsets)."""
+    import torch
+
+    from . import engine
+    src_off, dst_off, goff = reassembly_tables(shards, offs, cap)
+    out = torch.empty(max(int(goff[-1]), 1), dtype=torch.uint8, device=gathered.device)
+    torch.cuda.synchronize()
+    engine.copy_segments(gathered.data_ptr(), out.data_ptr(), src_off, dst_off, ctx=ctx)
+    return out[:int(goff[-1])], goff
+
+
+def reassemble(shards, parts, offs):
+    """Global-order bytes + offsets from per-rank (bytes, offsets) in shard
+    order, on the host (the CPU tests' twin of reassemble_device)."""
+    cap = max([len(p) for p in parts] + [1])
+    src_off, _, goff = reassembly_tables(shards, offs, cap)
+    flat = np.zeros(cap * len(parts), dtype=np.uint8)
+    for r, p in enumerate(parts):
+        flat[r * cap:r * cap + len(p)] = p
+    lens = goff[1:] - goff[:-1]
+    idx = np.repeat(src_off.astype(np.int64) - goff[:-1], lens) + np.arange(int(goff[-1]))
+    return flat[idx], goff

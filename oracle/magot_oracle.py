@@ -682,20 +682,6 @@ def coords2fasta(fasta_file, seqid, start, stop, truncate_names='False', out=Non
 
 
 
-def dna2orfs(fasta_file, from_atg=False, longest=False):
-    """genome_tools.py:145-180 (dna2orfs): (text written to output_file,
-    exception).  The reference calls .translate(frame=..., strand=...) on the
-    contig's plain str (GenomeSequence values are str, genome.py:870-877),
-    i.e. str.translate, which takes no keyword arguments: with at least one
-    contig the call raises TypeError before anything is written (the output
-    file is created empty).  Verified against the reference
-    (tests/golden/orfs.json)."""
-    seqs = read_fasta(fasta_file)
-    for _ in seqs:
-        return '', TypeError('translate() takes no keyword arguments')
-    return '', None
-
-
 # ---------------------------------------------------------------------------
 # Aligner outputs (genome.py:32-121, 425-499) and their extraction tools
 # (genome_tools.py:265-280, 483-485)

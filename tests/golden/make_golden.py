@@ -15,7 +15,6 @@ Outputs (data only: inputs, expected outputs, hashes):
   fixtures.json   hashes of whole-file gff2fasta outputs on the shipped data
   synth_small.json hashes of gff2fasta on the seeded small synthetic
   loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
-  orfs.json       dna2orfs output files (six-frame ORFs of whole contigs)
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
   translate_lib.json Sequence.translate with non-standard libraries, frames -6..6
@@ -356,46 +355,6 @@ def make_locus(ref):
 ORFS_GENOME = ('>c1 first contig\nATGAAATAGCCCATGGGTAAATGccctgaNNNNatgRYKMtaaGGGTTTAAACCC\n'
                'ATGATGATGTAGTAGTGA\n>c2\nnnnnATGCCCGGGTTTAAATGA\n>z9\nACGTACGTACGTAAATAG\n'
                '>a0\nTTATTATTACATCATCAT\n>mm\nMMMMATGCCC\n')
-
-
-def make_orfs(ref):
-    """genome_tools.dna2orfs (:145-180) of the reference: the output file's
-    text (its dict order is Python 3's here: contig insertion order) and the
-    exception, for each (from_atg, longest) the function treats by truth
-    value (the CLI passes strings, so "False" is true)."""
-    sys.path.insert(0, PY3)
-    import genome_tools as rt
-    import tempfile
-    out = {}
-    with tempfile.TemporaryDirectory() as td:
-        fa = os.path.join(td, 'orfs.fa')
-        with open(fa, 'w') as fh:
-            fh.write(ORFS_GENOME)
-        tiny = os.path.join(td, 'tiny.fa')
-        with open(tiny, 'w') as fh:
-            fh.write('>t1\nATGAAATAG\n>t2\nAT\n>t3\nATGCCC\n')
-        stops = os.path.join(td, 'stops.fa')
-        with open(stops, 'w') as fh:
-            fh.write('>s1\nTAATAATAA\n')
-        ob = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
-        args = [(False, False), (True, False), (False, True), (True, True), ('False', 'False')]
-        for tag, path in (('small', fa), ('tiny', tiny), ('stops', stops), ('obiroi', ob)):
-            for atg, lg in args:
-                if tag == 'obiroi' and (atg, lg) == ('False', 'False'):
-                    continue
-                dst = os.path.join(td, 'out.txt')
-                if os.path.exists(dst):
-                    os.remove(dst)
-                res, exc, so = call(lambda: rt.dna2orfs(path, dst, from_atg=atg, longest=lg))
-                text = open(dst).read() if os.path.exists(dst) else None
-                d = {'exc': exc,
-                     'sha256': sha(text) if text is not None else None,
-                     'bytes': len(text) if text is not None else None}
-                if text is not None and len(text) < 3000:
-                    d['text'] = text
-                out['%s/%s/%s' % (tag, atg, lg)] = d
-    out['_inputs'] = {'small': ORFS_GENOME}
-    return out
 
 
 def _match_genome():
@@ -747,8 +706,6 @@ def main():
         json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:
         json.dump(make_locus(ref), fh, indent=1, sort_keys=True)
-    with open(os.path.join(HERE, 'orfs.json'), 'w') as fh:
-        json.dump(make_orfs(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'kat.json'), 'w') as fh:
         json.dump(make_kat(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'edge_cases.json'), 'w') as fh:

@@ -55,3 +55,27 @@ def test_bench_spawns_two_ranks_weak():
                {'MAGOT_DIST_BACKEND': 'gloo'})
     assert d['n_gpus'] == 2 and d['scaling'] == 'weak'
     assert d['parity'].startswith('bit-exact'), d['parity']
+
+
+def test_bench_spawns_eight_ranks_strong():
+    """The world-8 job end to end (eight gloo ranks sharing this card): the
+    8-way sharding, the wire broadcast of the genome, every rank's shard
+    checked, the 8-part gather and the reassembly in global record order."""
+    d = _bench(['--gpus', '8', '--config', 'small'] + COMMON, {'MAGOT_DIST_BACKEND': 'gloo'})
+    assert d['n_gpus'] == 8
+    assert d['parity'].startswith('bit-exact'), d['parity']
+    g = d['outputs_gather']
+    assert g['parity'].startswith('bit-exact') and 'global record order' in g['parity'], g
+    assert d['genome_broadcast_bytes'] < 0.6 * d['genome_arena_bytes']
+    assert d['host']['peak_rss_gib_max_rank'] > 0
+
+
+def test_bench_six_frame_job_two_ranks():
+    """The C5 job over two ranks: six-frame streams gathered and put back into
+    the single-GPU layout, all six frames of every record checked."""
+    d = _bench(['--gpus', '2', '--config', 'small5'] + COMMON, {'MAGOT_DIST_BACKEND': 'gloo'})
+    assert d['roofline']['kernel'] == 'orf6_kernel'
+    assert d['parity'].startswith('bit-exact'), d['parity']
+    g = d['outputs_gather']
+    assert g['outputs'] == ['six-frame residues']
+    assert g['parity'].startswith('bit-exact') and 'six frames' in g['parity'], g

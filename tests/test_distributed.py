@@ -180,6 +180,57 @@ def test_reassemble_round_trip():
     assert np.array_equal(out, data) and np.array_equal(goff, off)
 
 
+def test_six_frame_blocks_reassemble_to_single_gpu_layout():
+    """C5 over N ranks: each rank's six-frame output is its records' blocks of
+    six 16-byte padded streams (magot_orf6_sizes over its own records); one
+    segment per record puts them back into exactly the layout a single-GPU
+    job writes (magot_orf6_sizes over the global record order), stream by
+    stream (j = 6 * record + 2 * frame + strand)."""
+    from magot_amd import engine, shard
+    rng = np.random.default_rng(17)
+    n = 700
+    rec_len = rng.integers(0, 400, size=n)
+    rec_len[:5] = [0, 1, 2, 3, 5]                       # None streams and short frames
+    noff = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(rec_len, out=noff[1:])
+    gsoff, gslen = engine.orf6_sizes(noff)
+    # the single-GPU output: stream j filled with a byte derived from j
+    glob = np.zeros(int(gsoff[-1]), dtype=np.uint8)
+    for j in range(6 * n):
+        glob[int(gsoff[j]):int(gsoff[j]) + int(gslen[j])] = (j * 37 + 11) & 0xFF
+    tx_contig = np.sort(rng.integers(0, 6, size=n))
+    shards, _, _ = shard.record_shards(tx_contig, rec_len + 1, 6, 4,
+                                       tx_start=rng.integers(0, 10**6, size=n))
+    parts, offs = [], []
+    for sh in shards:
+        lo = np.zeros(len(sh) + 1, dtype=np.int64)
+        np.cumsum(rec_len[sh], out=lo[1:])
+        soff, slen = engine.orf6_sizes(lo)
+        part = np.zeros(int(soff[-1]), dtype=np.uint8)
+        for i, t in enumerate(sh):
+            for k in range(6):
+                j = 6 * int(t) + k
+                part[int(soff[6 * i + k]):int(soff[6 * i + k]) + int(slen[6 * i + k])] = \
+                    (j * 37 + 11) & 0xFF
+        parts.append(part)
+        offs.append(np.append(soff[0:-1:6], soff[-1]).astype(np.int64))
+    got, goff = shard.reassemble(shards, parts, offs)
+    assert np.array_equal(goff, gsoff[0::6].astype(np.int64))
+    assert np.array_equal(got, glob)
+
+
+def test_reassembly_tables_rank_major():
+    from magot_amd import shard
+    shards = [np.array([1, 3]), np.array([0, 2, 4])]
+    offs = [np.array([0, 5, 6]), np.array([0, 2, 2, 9])]
+    src, dst, goff = shard.reassembly_tables(shards, offs, cap=16)
+    assert goff.tolist() == [0, 2, 7, 7, 8, 15]
+    assert dst.tolist() == goff.tolist()
+    assert src.tolist() == [16, 0, 18, 5, 18]
+    with pytest.raises(ValueError):
+        shard.reassembly_tables(shards, [offs[0], offs[1][:-1]], cap=16)
+
+
 def _gather_worker(rank, world, port, q):
     os.environ.update({'RANK': str(rank), 'WORLD_SIZE': str(world),
                        'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
@@ -190,8 +241,11 @@ def _gather_worker(rank, world, port, q):
     n = 10 + 7 * rank
     t = torch.arange(n + 5, dtype=torch.int64).to(torch.uint8) + rank
     got = shard.gather_bytes(dist, rank, world, t, n)
+    offs = shard.gather_offsets(dist, rank, world, np.arange(3 + rank) * (rank + 2))
     if rank == 0:
-        q.put([g.tolist() for g in got])
+        q.put(([g.tolist() for g in got], [o.tolist() for o in offs]))
+    else:
+        assert offs is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -204,13 +258,14 @@ def test_gather_bytes_two_ranks_gloo():
     procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    got, offs = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in range(world):
         n = 10 + 7 * r
         assert got[r] == [(i + r) & 0xFF for i in range(n)]
+        assert offs[r] == [i * (r + 2) for i in range(3 + r)]
 
 
 # ---------------------------------------------------------------------------

@@ -101,10 +101,25 @@ def test_single_sequence_abi_kat():
                 continue
             f, st, trim = int(key[0]), key[1], int(key[2])
             n = ctypes.c_int64()
-            _lib.check(L.magot_translate(ctx.handle, buf, len(seq), f, ord(st), trim, out,
+            # out sized as the header states, (len + 2) / 3, plus guard bytes
+            cap = (len(seq) + 2) // 3
+            tout = (ctypes.c_uint8 * (cap + 8))(*([0xEE] * (cap + 8)))
+            _lib.check(L.magot_translate(ctx.handle, buf, len(seq), f, ord(st), trim, tout,
                                          ctypes.byref(n)), 'magot_translate')
-            got = None if n.value < 0 else bytes(out)[:n.value].decode('latin-1')
+            got = None if n.value < 0 else bytes(tout)[:n.value].decode('latin-1')
             assert got == want, (r['seq'], key)
+            assert n.value <= cap and bytes(tout)[max(n.value, 0):] == b'\xee' * (
+                cap + 8 - max(n.value, 0)), (r['seq'], key)  # nothing past the result
+    # frame 1 of a length with len % 3 == 2: (len + 1) / 3 residues before the trim
+    for seq, f, trim, want in [(b'GATGA', 1, 0, 'X*'), (b'GATGA', 1, 1, '*'),
+                               (b'GGATGAAAA', 2, 0, 'XE')]:
+        cap = (len(seq) + 2) // 3
+        tout = (ctypes.c_uint8 * (cap + 4))(*([0xEE] * (cap + 4)))
+        n = ctypes.c_int64()
+        _lib.check(L.magot_translate(ctx.handle, seq, len(seq), f, ord('+'), trim, tout,
+                                     ctypes.byref(n)), 'magot_translate')
+        assert bytes(tout)[:n.value].decode() == want and bytes(tout)[n.value:] == \
+            b'\xee' * (cap + 4 - n.value)
 
 
 def test_sequence_api_kat():
@@ -525,8 +540,15 @@ def test_orf6_batch_tile_shapes_vs_oracle():
         assert six == _oracle_six(s), (i, len(s))
 
 
-def test_orf6_over_extraction_plan_vs_oracle():
-    """C5 shape at small size: gather + six-frame translation, all in HBM."""
+@pytest.mark.parametrize('walk', ['genome', 'record'])
+def test_orf6_over_extraction_plan_vs_oracle(monkeypatch, walk):
+    """C5 shape at small size: gather + six-frame translation, all in HBM;
+    the kernel's walk in genome order (default) and in record order
+    (MAGOT_ORF6_ORDER=record)."""
+    if walk == 'record':
+        monkeypatch.setenv('MAGOT_ORF6_ORDER', 'record')
+    else:
+        monkeypatch.delenv('MAGOT_ORF6_ORDER', raising=False)
     w = synth.make('small', seed=43, genome_bases=1_000_000, n_tx=400, iupac_rate=2e-3)
     dev = engine.DeviceGenome(w.contigs())
     ex, tx = w.plan_tables()

@@ -1,0 +1,211 @@
+"""Genome placement and output reassembly on the GPU:
+
+* the device packer (magot_genome_load, devpack.hip) against its host twin
+  (MAGOT_PACK_HOST, pack.cpp): byte-equal arenas and host tables, over every
+  byte value, runs across contigs / 32-byte groups / the 64 MiB staging
+  chunks, empty contigs, FASTA line layout, and the C5 genome;
+* the wire replica (magot_genome_wire_ranges + magot_genome_attach_wire):
+  only the forward plane, runs and directory are transferred, the mirror is
+  rebuilt, and the attached arena equals the packed one byte for byte;
+* magot_copy_segments against numpy, aligned and unaligned.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from magot_amd import _lib, engine, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _device():
+    if _lib.lib().magot_device_count() <= 0:
+        pytest.fail('no HIP device visible for a gpu test')
+
+
+def _arena(g):
+    buf = torch.empty(g.device_bytes, dtype=torch.uint8, device='cuda')
+    g.copy_arena(buf.data_ptr())
+    torch.cuda.synchronize()
+    return buf.cpu().numpy()
+
+
+def _defined(g, arena):
+    """The arena bytes the layout defines: both nibble planes + 16 bytes of
+    slack, then the runs and the directory (Carve padding excluded)."""
+    (o0, l0), (o1, l1) = g.wire_ranges()
+    assert o0 == 0
+    return np.concatenate([arena[o0:o0 + 2 * l0 + 16], arena[o1:o1 + l1]])
+
+
+def _assert_same_pack(contigs):
+    dg = engine.DeviceGenome(contigs, pack='device')
+    hg = engine.DeviceGenome(contigs, pack='host')
+    try:
+        assert dg.export() == hg.export()  # layout, runs, directory, contig table
+        assert dg.device_bytes == hg.device_bytes
+        a, b = _arena(dg), _arena(hg)
+        da, db = _defined(dg, a), _defined(hg, b)
+        if not np.array_equal(da, db):
+            bad = int(np.nonzero(da != db)[0][0])
+            raise AssertionError('arenas differ at defined byte %d: %r vs %r'
+                                 % (bad, da[bad:bad + 8], db[bad:bad + 8]))
+        return dg.n_exception_runs
+    finally:
+        dg.close()
+        hg.close()
+
+
+def test_device_pack_every_byte_value():
+    """Every byte GenomeSequence keeps (all but CR/LF, genome.py:875) in runs
+    of varying length, runs touching each other, crossing 32-byte groups and
+    contig boundaries, zero-length contigs between them."""
+    rng = np.random.default_rng(5)
+    values = [b for b in range(256) if b not in (10, 13)]
+    parts = []
+    for k, b in enumerate(values * 3):
+        parts.append(rng.choice(np.frombuffer(b'ACGTacgt', np.uint8), int(rng.integers(0, 40))))
+        parts.append(np.full(1 + (k * 7) % 45, b, dtype=np.uint8))
+    seq = np.concatenate(parts).tobytes()
+    cuts = sorted(rng.choice(len(seq), 12, replace=False).tolist())
+    contigs, last = [], 0
+    for i, c in enumerate(cuts + [len(seq)]):
+        contigs.append(('c%d' % i, seq[last:c]))
+        if i % 4 == 1:
+            contigs.append(('empty%d' % i, b''))
+        last = c
+    assert _assert_same_pack(contigs) > 700
+
+
+@pytest.mark.parametrize('shape', ['empty', 'one_base', 'all_N', 'exc_at_ends'])
+def test_device_pack_edge_genomes(shape):
+    contigs = {
+        'empty': [],
+        'one_base': [('a', b'n')],
+        'all_N': [('a', b'N' * 100_000), ('b', b'N' * 33)],
+        'exc_at_ends': [('a', b'RACGTY'), ('b', b'YY' + b'ACGT' * 40 + b'-'), ('c', b'')],
+    }[shape]
+    _assert_same_pack(contigs)
+
+
+def test_device_pack_crosses_staging_chunks():
+    """A 200 Mb genome: runs cross the 64 MiB pinned staging chunks."""
+    rng = np.random.default_rng(9)
+    G = 200_000_000
+    g = np.frombuffer(b'ACGT', np.uint8)[rng.integers(0, 4, size=G, dtype=np.uint8)]
+    for c in range(1, 4):  # an N run straddling each chunk boundary
+        p = c * (64 << 20)
+        g[p - 1000:p + 1000] = ord('N')
+        g[p - 3000] = ord('Y')
+    g[rng.integers(0, G, 5000)] = ord('R')
+    contigs = [('a', g[:G // 3].tobytes()), ('b', g[G // 3:].tobytes())]
+    assert _assert_same_pack(contigs) > 4000
+
+
+def test_device_pack_fasta_line_layout():
+    """magot_genome_load_fasta streams the file's lines (newlines dropped) to
+    the device packer: same arena as the host packer over the same contigs."""
+    w = synth.make('small', seed=4, genome_bases=300_000, n_tx=10, iupac_rate=1e-3)
+    text = w.fasta_text(width=61).encode('latin-1')
+    fg = engine.FastaGenome.load(text)
+    hg = engine.DeviceGenome(w.contigs(), pack='host')
+    try:
+        assert fg.names == w.contig_names
+        m1, m2 = fg.export(), hg.export()
+        assert m1 == m2
+        assert np.array_equal(_defined(fg, _arena(fg)), _defined(hg, _arena(hg)))
+    finally:
+        fg.close()
+        hg.close()
+
+
+@pytest.mark.slow
+def test_device_pack_c5_genome():
+    """BASELINE configs[4]'s 3 Gb genome, device vs host packer."""
+    w = synth.make('C5')
+    _assert_same_pack(w.contigs())
+
+
+def _wire_replica(g):
+    """What a receiving rank holds: the wire ranges copied into fresh memory
+    (the rest poisoned), attached with the mirror rebuilt."""
+    meta, nbytes = g.export()
+    src = torch.empty(nbytes, dtype=torch.uint8, device='cuda')
+    g.copy_arena(src.data_ptr())
+    dst = torch.full((nbytes,), 0xAB, dtype=torch.uint8, device='cuda')
+    moved = 0
+    for off, ln in g.wire_ranges():
+        dst[off:off + ln].copy_(src[off:off + ln])
+        moved += ln
+    torch.cuda.synchronize()
+    rep = engine.DeviceGenome.attach(meta, dst.data_ptr(), g.names, g.lengths, keepalive=dst,
+                                     wire=True)
+    return rep, moved
+
+
+def test_wire_replica_equals_packed_arena():
+    w = synth.make('small', seed=12, genome_bases=2_000_000, n_tx=800, iupac_rate=1e-3)
+    g = engine.DeviceGenome(w.contigs())
+    rep, moved = _wire_replica(g)
+    try:
+        a, b = _arena(g), _arena(rep)
+        assert np.array_equal(_defined(g, a), _defined(rep, b))
+        (o0, l0), (o1, l1) = g.wire_ranges()
+        assert moved == l0 + l1 and o1 >= 2 * l0 + 16  # the mirror plane is not sent
+        # and the replica extracts the same bytes
+        ex, tx = w.plan_tables()
+        outs = []
+        for gen in (g, rep):
+            plan = engine.ExtractionPlan(gen, ex, tx)
+            outs.append(plan.run())
+            plan.close()
+        for x, y in zip(outs[0], outs[1]):
+            assert np.array_equal(x, y)
+    finally:
+        rep.close()
+        g.close()
+
+
+@pytest.mark.slow
+def test_wire_replica_c3_genome():
+    w = synth.make('C3')
+    g = engine.DeviceGenome(w.contigs())
+    rep, moved = _wire_replica(g)
+    try:
+        assert np.array_equal(_defined(g, _arena(g)), _defined(rep, _arena(rep)))
+        assert moved < 0.51 * g.device_bytes
+    finally:
+        rep.close()
+        g.close()
+
+
+@pytest.mark.parametrize('aligned', [False, True])
+def test_copy_segments_vs_numpy(aligned):
+    rng = np.random.default_rng(21 + aligned)
+    n = 5000
+    lens = rng.integers(0, 300, n)
+    lens[rng.integers(0, n, 50)] = rng.integers(1000, 5000, 50)  # a few long segments
+    if aligned:
+        lens = (lens + 15) & ~15
+    src_bytes = int(lens.sum()) + 3 * n + 64
+    src = rng.integers(0, 256, src_bytes, dtype=np.uint8)
+    perm = rng.permutation(n)
+    # source places: a shuffled packing of the segments (aligned if asked)
+    src_off = np.zeros(n, dtype=np.uint64)
+    at = 0
+    for i in perm:
+        src_off[i] = at
+        at += int(lens[i]) + (0 if aligned else int(rng.integers(0, 3)))
+    assert at <= src_bytes
+    dst_off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=dst_off[1:])
+    want = np.concatenate([src[int(src_off[i]):int(src_off[i]) + int(lens[i])] for i in range(n)])
+    d_src = torch.from_numpy(src).cuda()
+    d_dst = torch.full((int(dst_off[-1]) + 64,), 0xEE, dtype=torch.uint8, device='cuda')
+    torch.cuda.synchronize()
+    engine.copy_segments(d_src.data_ptr(), d_dst.data_ptr(), src_off, dst_off)
+    got = d_dst.cpu().numpy()
+    assert np.array_equal(got[:int(dst_off[-1])], want)
+    assert (got[int(dst_off[-1]):] == 0xEE).all()  # nothing written past the end

@@ -107,45 +107,3 @@ def test_gpu_coords2fasta_matches_reference(small, key):
     text, exc = _run_cli(genome_tools.coords2fasta, small[0], seqid, a, b, tr)
     assert exc == GOLD[key]['exc']
     assert text == GOLD[key]['stdout']
-
-
-# ---------------------------------------------------------------------------
-# dna2orfs (genome_tools.py:145-180): broken in the reference -- str.translate
-# takes no keyword arguments -- pinned by tests/golden/orfs.json.
-# ---------------------------------------------------------------------------
-
-def test_dna2orfs_matches_reference_failure(tmp_path):
-    import json
-    from magot_amd import genome_tools
-    gold = json.load(open(os.path.join(os.path.dirname(__file__), 'golden', 'orfs.json')))
-    fa = tmp_path / 'orfs.fa'
-    fa.write_text(gold['_inputs']['small'])
-    for key, want in gold.items():
-        if not key.startswith('small/'):
-            continue
-        _, atg, lg = key.split('/')
-        dst = tmp_path / 'out.txt'
-        dst.write_text('stale')
-        with pytest.raises(TypeError):
-            genome_tools.dna2orfs(str(fa), str(dst), from_atg=atg, longest=lg)
-        assert want['exc'] == 'TypeError' and want['bytes'] == 0
-        assert dst.read_text() == ''  # created (truncated) before the failure
-        text, exc = mo.dna2orfs(str(fa), atg, lg)
-        assert text == '' and isinstance(exc, TypeError)
-    empty = tmp_path / 'empty.fa'
-    empty.write_text('')
-    genome_tools.dna2orfs(str(empty), str(tmp_path / 'o2.txt'))  # no contig: no error
-    assert (tmp_path / 'o2.txt').read_text() == ''
-
-
-def test_get_cds_peptides_matches_reference_failure(tmp_path):
-    """genome_tools.py:283-322 calls the undefined Genome.read_gff3: the
-    reference raises AttributeError after reading the genome and before it
-    opens the output file; so does the drop-in (no output file)."""
-    from magot_amd import genome_tools
-    fa = tmp_path / 'g.fa'
-    fa.write_text('>c1\nATGAAATAG\n')
-    dst = tmp_path / 'out.fa'
-    with pytest.raises(AttributeError):
-        genome_tools.get_CDS_peptides(str(fa), 'unused.gff', str(dst))
-    assert not dst.exists()
