@@ -191,6 +191,82 @@ def settle(fn, sync, ms):
 
 
 # ---------------------------------------------------------------------------
+# Box state (C5's fast and slow states): amd-smi counters around
+# the timed region and a memory-system probe in this process
+# ---------------------------------------------------------------------------
+
+_SMI_FIELDS = [('used_vram_mb', r'USED_VRAM: (\d+) MB'), ('socket_power_w', r'SOCKET_POWER: (\d+) W'),
+               ('umc_activity_pct', r'UMC_ACTIVITY: (\d+) %'),
+               ('hotspot_c', r'HOTSPOT: (\d+)'), ('mem_temp_c', r'\n\s+MEM: (\d+)'),
+               ('mem_clk_mhz', r'MEM_0:\s+CLK: (\d+) MHz'), ('fclk_mhz', r'FCLK_0:\s+CLK: (\d+) MHz'),
+               ('energy_j', r'TOTAL_ENERGY_CONSUMPTION: ([\d.]+) J'),
+               ('acc_counter', r'ACCUMULATION_COUNTER: (\d+)'),
+               ('ppt_acc', r'PPT_ACCUMULATED: (\d+)'),
+               ('socket_thermal_acc', r'SOCKET_THERMAL_ACCUMULATED: (\d+)'),
+               ('vr_thermal_acc', r'VR_THERMAL_ACCUMULATED: (\d+)'),
+               ('hbm_thermal_acc', r'HBM_THERMAL_ACCUMULATED: (\d+)'),
+               ('prochot_acc', r'PROCHOT_ACCUMULATED: (\d+)')]
+
+
+def smi_snapshot(device):
+    """A few amd-smi metric fields of `device` (None when amd-smi is not
+    there).  A child process, never an exec."""
+    import re
+    try:
+        r = subprocess.run(['amd-smi', 'metric', '-g', str(device)], capture_output=True,
+                           text=True, timeout=20)
+    except Exception:
+        return None
+    if r.returncode != 0:
+        return None
+    out = {'t': time.time()}
+    for key, pat in _SMI_FIELDS:
+        m = re.search(pat, r.stdout)
+        if m:
+            out[key] = float(m.group(1))
+    return out
+
+
+def memory_probe(nbytes=4 << 30, iters=5):
+    """Streaming store and copy bandwidth of this device now (torch fill_ /
+    copy_ of `nbytes`, timed with events on torch's stream): the memory
+    system's state in the process that measures the kernel (C5's slow state
+    slows a pure store replay as much as the kernel)."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device='cuda')
+    b = torch.empty(nbytes // 2, dtype=torch.uint8, device='cuda')
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    res = {}
+    for name, fn, moved in (('store_gbs', lambda: a.fill_(7), nbytes),
+                            ('copy_gbs', lambda: b.copy_(a[:nbytes // 2]), nbytes)):
+        fn()
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        res[name] = moved * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return res
+
+
+def box_state(device, before, after, probe_before, probe_after):
+    """The run's box record: counter deltas over the timed region, the probes,
+    and the used VRAM before the job (another tenant's memory shows here)."""
+    st = {'probe_before': probe_before, 'probe_after': probe_after}
+    if before and after:
+        st['smi_before'] = before
+        st['smi_after'] = after
+        st['delta'] = {k: after[k] - before[k] for k in
+                       ('energy_j', 'acc_counter', 'ppt_acc', 'socket_thermal_acc',
+                        'vr_thermal_acc', 'hbm_thermal_acc', 'prochot_acc', 't')
+                       if k in before and k in after}
+    return st
+
+
+# ---------------------------------------------------------------------------
 # CPU baseline: the reference's per-record loop (CPU oracle restatement of
 # genome.py:603-822), single core, on a bounded sample of the same workload.
 # ---------------------------------------------------------------------------
@@ -456,6 +532,10 @@ def run_job(args, dist, rank, local, world):
             else 'MISMATCH on %d rank(s)' % int(n_bad)
 
     # -- timed region ---------------------------------------------------------
+    record_box = rank == 0 and not args.no_box_state
+    if record_box:
+        smi0 = smi_snapshot(local)
+        probe0 = memory_probe()
     settled = settle(step, ctx.sync, args.settle_ms)
     launches_before += settled['launches'] + args.warmup
     for _ in range(args.warmup):
@@ -482,6 +562,9 @@ def run_job(args, dist, rank, local, world):
     kernel_b2b = timer.time_b2b(n_b2b)
     kernel_iso = timer.time(10)
     kernel_ms_max = allreduce_max(dist, kernel_ms)
+    boxrec = None
+    if record_box:
+        boxrec = box_state(local, smi0, smi_snapshot(local), probe0, memory_probe())
     total_bases = allreduce_sum(dist, float(B))
     alg_mean = allreduce_sum(dist, float(alg)) / world
     value = total_bases * args.steps / elapsed_max
@@ -586,6 +669,7 @@ def run_job(args, dist, rank, local, world):
             'parity': parity,
             'phases_s': phases,
             'host': host,
+            'box_state': boxrec,
             'outputs_d2h_bases_per_s': total_bases / t_d2h if t_d2h else None,
             'output_bytes_rank0': out_bytes,
         }
@@ -698,6 +782,8 @@ def main(argv=None):
                          '(default, SURVEY 8(d)) or coordinate-sorted (diagnostic)')
     ap.add_argument('--no-verify', action='store_true', help='skip the oracle byte check')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-box-state', action='store_true',
+                    help='skip the amd-smi snapshots and memory probes around the timed region')
     ap.add_argument('--cpu-sample-bases', type=float, default=1.0e8)
     ap.add_argument('--pmc-json', default=None,
                     help='per-launch HBM traffic measured with rocprofv3 --pmc '

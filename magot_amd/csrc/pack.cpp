@@ -158,7 +158,11 @@ void exc_runs_directory(HostPacked* out) {
 
 void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out) {
   pack_layout(src, n, out);
-  out->nib.reset(new uint32_t[out->nib_words]);  // written in full by the pieces
+  out->nib.reset(new uint32_t[out->nib_words]);  // written in full by the pieces, except
+  // the words of the kOrigin pad bases, which no piece reaches (the first
+  // contig starts at kOrigin): zero them here (the device packer's arena
+  // matched everywhere but these seven words, tests/test_gpu_replication.py)
+  for (uint64_t w = 0; w < std::min<uint64_t>(kOrigin / 8, out->nib_words); ++w) out->nib[w] = 0;
 
   // Split [0, span) into 32-aligned pieces for the worker threads.
   unsigned hw = std::max(1u, std::min(32u, std::thread::hardware_concurrency()));

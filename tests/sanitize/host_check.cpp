@@ -134,6 +134,9 @@ static void check_pack(const std::vector<ContigSource>& src) {
   for (uint64_t g = hp.extent; g < hp.span; ++g)
     CHECK(((hp.nib[g >> 3] >> (4 * (g & 7))) & 15u) == 0, "padding nibble at %llu",
           (unsigned long long)g);
+  for (uint64_t g = 0; g < kOrigin && g < hp.span; ++g)  // the leading pad too
+    CHECK(((hp.nib[g >> 3] >> (4 * (g & 7))) & 15u) == 0, "leading pad nibble at %llu",
+          (unsigned long long)g);
   // directory: first run whose end lies past the block start
   for (size_t b = 0; b < hp.dir.size(); ++b) {
     const uint64_t bs = (uint64_t)b << kDirShift;

@@ -37,6 +37,12 @@ def test_bench_one_rank():
     assert d['parity'].startswith('bit-exact'), d['parity']
     assert d['value'] > 0 and d['roofline']['kernel_ms'] > 0
     assert d['phases_s']['outputs_d2h_pinned'] > 0
+    # kernel time from events around exactly the K timed launches
+    tl = d['roofline']['timed_launches']
+    assert tl['count'] == 5 and tl['first'] == 1 + d['settle']['launches'] + 1
+    assert d['roofline']['kernel_ms'] <= d['ms_per_step'] * 1.05
+    probe = d['box_state']['probe_before']
+    assert probe['store_gbs'] > 100 and probe['copy_gbs'] > 100
 
 
 def test_bench_spawns_two_ranks_strong():

@@ -640,6 +640,58 @@ def test_orf6_fused_gather_tiny_intervals_vs_oracle():
     dev.close()
 
 
+def test_orf6_intervals_at_plane_edges_vs_oracle():
+    """Six frames of records whose intervals touch the first and last bases of
+    the genome plane on both strands ('-' intervals are read backwards from
+    the forward planes, so their windows run to the plane's two ends), with
+    exceptions right at the edges; single- and multi-interval records."""
+    rng = np.random.default_rng(77)
+    acgt = np.frombuffer(b'ACGTacgt', np.uint8)
+    first = b'NR' + rng.choice(acgt, 500).tobytes() + b'YN'
+    mid = rng.choice(acgt, 3000).tobytes()
+    last = rng.choice(acgt, 700).tobytes() + b'KMn'
+    contigs = [('a', first), ('b', mid), ('c', last)]
+    text = [c.decode('latin-1') for _, c in contigs]
+    dev = engine.DeviceGenome(contigs)
+    rows, txs, want = [], [], []
+    for t in range(300):
+        n = 1 + t % 4
+        minus = bool(t % 2)
+        b = len(rows)
+        segs = []
+        for k in range(n):
+            c = 0 if (t + k) % 3 == 0 else 2
+            L = len(contigs[c][1])
+            ln = int(rng.integers(1, 60)) if t % 5 else int(rng.integers(100, L))
+            st = 0 if (t // 2) % 2 == 0 else L - ln  # at the contig's first / last base
+            rows.append(((st | (1 << 63)) if minus else st, c, ln))
+            seg = text[c][st:st + ln]
+            segs.append(mo.reverse_complement(seg) if minus else seg)
+        txs.append((b, n, 0))
+        want.append(''.join(segs))
+    ex = np.array(rows, dtype=engine.EXON_DTYPE)
+    tx = np.array(txs, dtype=engine.TX_DTYPE)
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    nuc, noff, _, _ = plan.run()
+    for r, s in enumerate(want):
+        assert nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1') == s, r
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    raw = out.tobytes().decode('latin-1')
+    for r, s in enumerate(want):
+        six = _oracle_six(s)
+        for k in range(6):
+            j = 6 * r + k
+            got = raw[int(soff[j]):int(soff[j] + slen[j])]
+            if k < 2 and got[:1] == 'X':
+                got = got[1:]
+            assert got == (six[k] or ''), (r, k, s)
+    o6.close()
+    plan.close()
+    dev.close()
+
+
 def test_every_byte_class_both_strands_vs_oracle():
     """Every printable byte GenomeSequence keeps (genome.py:875) inside CDS
     intervals on both strands: the literal classes the kernels decode from
