@@ -485,11 +485,11 @@ def run_job(args, dist, rank, local, world):
         log('%d records over %d ranks: load imbalance %.4f%%, %d contig(s) split'
             % (w.n_tx, world, 100.0 * imb, int((spans[:, 0] != spans[:, 1]).sum())))
         dev, t_bcast, bcast_bytes = shard.replicate_genome(
-            dist, rank, w.contigs() if rank == 0 else None, ctx)
+            dist, rank, w.contig_views() if rank == 0 else None, ctx)
         t_bcast = allreduce_max(dist, t_bcast)
     else:
         t0 = time.perf_counter()
-        dev = engine.DeviceGenome(w.contigs(), ctx=ctx)
+        dev = engine.DeviceGenome(w.contig_views(), ctx=ctx)
         t_pack = time.perf_counter() - t0
 
     ex, tx = w.plan_tables(tx_subset=mine)

@@ -1482,12 +1482,10 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
     return rc;
   o->total = o->host_soff.back();
   const uint64_t total_nuc = p->nuc_off.back();
-  // interval rows {forward anchor, start | flags} from the plan's compacted
-  // table: every interval reads the FORWARD planes (a '-' interval reads its
-  // span backwards and the kernel reverse-complements in registers), so the
-  // six-frame planes cover one strand and overlapping '+' and '-' records
-  // share their genome lines in L2.  Concatenation position P of a '+'
-  // interval is forward base anchor + P, of a '-' interval anchor - P.
+  // interval rows {unified anchor, start} from the plan's compacted table
+  // (a '-' interval reads the mirror plane forward; staging every interval
+  // from the forward planes instead, '-' read backwards and reverse-
+  // complemented in registers, measured 5 % slower: DESIGN.md 3, round 4)
   const uint64_t ne = p->n_ex_c;
   std::vector<uint64_t> ex_g(ne), ex_out(ne + 1), rows(2 * (ne + 1));
   if (ne) {
@@ -1499,16 +1497,10 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   for (uint64_t i = 0; i < ne; ++i) {
     const uint64_t gw = ex_g[i], o0 = ex_out[i], len = ex_out[i + 1] - o0;
     const uint64_t gs = gw & ~kExFlagBits;
-    const bool rc = (gw & kRcBit) != 0;
-    rows[2 * i] = rc ? gs + len - 1 + o0 : gs - o0;
-    rows[2 * i + 1] = o0 | ((gw & kExcBit) ? kOrf6ExcRow : 0ull) | (rc ? kOrf6RevRow : 0ull);
+    rows[2 * i] = (gw & kRcBit) ? 2 * span - gs - len - o0 : gs - o0;
+    rows[2 * i + 1] = o0 | ((gw & kExcBit) ? kOrf6ExcRow : 0ull);  // the exact path's flag
     starts[i] = o0;
   }
-  (void)span;
-  // forward base of concatenation position starts[e] (the interval's first)
-  auto fwd_first = [&](uint64_t e) {
-    return (rows[2 * e + 1] & kOrf6RevRow) ? rows[2 * e] - starts[e] : rows[2 * e] + starts[e];
-  };
   rows[2 * ne] = 0;
   rows[2 * ne + 1] = total_nuc;
   starts[ne] = total_nuc;
@@ -1534,7 +1526,8 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
       }
       ie[n] = ne;
       for (uint64_t r = 0; r < n; ++r)
-        key[r] = noff[r + 1] > noff[r] && ie[r] < ie[r + 1] ? fwd_first(ie[r]) : ~0ull;
+        key[r] = noff[r + 1] > noff[r] && ie[r] < ie[r + 1] ? rows[2 * ie[r]] + starts[ie[r]]
+                                                             : ~0ull;
       for (uint64_t r = 0; r < n; ++r) perm[r] = r;
       std::stable_sort(perm.begin(), perm.end(),
                        [&](uint64_t x, uint64_t y) { return key[x] < key[y]; });
@@ -1557,10 +1550,8 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
             return MAGOT_ERR_STATE;
           }
           const uint64_t st_k = noff_k[k] + (st - noff[r]);
-          const bool rev = (rows[2 * e + 1] & kOrf6RevRow) != 0;
-          // the same forward bases at the new positions
-          rows_k[2 * j] = rev ? rows[2 * e] - st + st_k : rows[2 * e] + st - st_k;
-          rows_k[2 * j + 1] = st_k | (rows[2 * e + 1] & (kOrf6ExcRow | kOrf6RevRow));
+          rows_k[2 * j] = rows[2 * e] + st - st_k;  // the same unified anchor
+          rows_k[2 * j + 1] = st_k | (rows[2 * e + 1] & kOrf6ExcRow);
           starts_k[j] = st_k;
           ++j;
         }
@@ -1597,10 +1588,9 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   const uint64_t o_m = cv.take<uint32_t>(n_tiles);
   const uint64_t o_lut = cv.take<uint8_t>(256);
   const uint64_t nib_words = p->args.span / 4;  // forward + reverse planes, 8 bases per word
-  const uint64_t fwd_words = p->args.span / 8;  // the forward plane alone
-  const uint64_t code2_words = fwd_words / 2;
+  const uint64_t code2_words = nib_words / 2;
   const uint64_t o_code2 = cv.take<uint32_t>(code2_words + 4);
-  const uint64_t exc1_words = fwd_words / 4;
+  const uint64_t exc1_words = nib_words / 4;
   const uint64_t o_exc1 = cv.take<uint32_t>(exc1_words + 4);
   MAGOT_HIP_TRY(hipMalloc(&o->arena, cv.used));
   char* base = static_cast<char*>(o->arena);
@@ -1609,11 +1599,8 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   };
   uint32_t* code2 = reinterpret_cast<uint32_t*>(base + o_code2);
   uint32_t* exc1 = reinterpret_cast<uint32_t*>(base + o_exc1);
-  launch_code2(p->args.nib, fwd_words, code2, ctx->stream);
-  launch_exc1(p->args.nib, fwd_words, exc1, ctx->stream);
-  // the planes' slack words (window over-reads past the forward plane)
-  MAGOT_HIP_TRY(hipMemsetAsync(code2 + code2_words, 0, 16, ctx->stream));
-  MAGOT_HIP_TRY(hipMemsetAsync(exc1 + exc1_words, 0, 16, ctx->stream));
+  launch_code2(p->args.nib, nib_words, code2, ctx->stream);
+  launch_exc1(p->args.nib, nib_words, exc1, ctx->stream);
   MAGOT_HIP_TRY(hipGetLastError());
   MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   MAGOT_HIP_TRY(up(o_off, noff_k.data(), (o->n_rec + 1) * 8));

@@ -240,23 +240,20 @@ void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t
 // offsets; noff = n_rec+1 offsets of the records in the concatenation.
 // The records are either bytes (nuc, readable up to the next 16-byte
 // boundary) or gathered from the genome plane through interval rows
-// {forward anchor, start | flags} (n_rows + a sentinel row {0, total}): base
-// P of the concatenation is forward base anchor + P of its interval, or the
-// complement of forward base anchor - P for a kOrf6RevRow ('-') interval.
+// {unified anchor, start} (n_rows + a sentinel row {0, total}): base P of
+// the concatenation is unified coordinate anchor + P of its interval.
 // Tiles (orf6_plan_tiles): t0 = n_tiles+1 starts, r0 = record holding each
 // start, e0 = interval holding each staged window's first base.
 constexpr uint32_t kOrf6RowCap = 123;  // intervals per staged window
 constexpr uint64_t kOrf6ExcRow = 1ull << 63;  // row start flag: the interval touches an exception run
-constexpr uint64_t kOrf6RevRow = 1ull << 62;  // row start flag: '-' interval, read backwards
-                                              // from the forward planes (anchor - P)
 struct Orf6Args {
   const uint8_t* nuc;
   const uint32_t* nib;
   uint64_t nib_words;      // both planes
-  const uint32_t* code2;   // 2-bit codes of the forward plane's bases, 16 per word
-  uint64_t code2_words;    // = span / 16
-  const uint32_t* exc1;    // exception bits of the forward plane's bases, 32 per word
-  uint64_t exc1_words;     // = span / 32
+  const uint32_t* code2;   // 2-bit codes of the same unified bases, 16 per word
+  uint64_t code2_words;    // = nib_words / 2
+  const uint32_t* exc1;    // exception bits of the same unified bases, 32 per word
+  uint64_t exc1_words;     // = nib_words / 4
   const uint64_t* rows;
   uint64_t n_rows;
   const uint64_t* noff;

@@ -210,19 +210,6 @@ __device__ __forceinline__ uint32_t nib_codes(uint32_t x0, uint32_t x1) {
   return __builtin_amdgcn_perm(z1, z0, 0x06040200u);
 }
 
-// Sixteen packed 2-bit codes read backwards and complemented (a '-' interval
-// staged from the forward plane): code j of the result is 3 - code 15 - j.
-__device__ __forceinline__ uint32_t rc_codes(uint32_t x) {
-  const uint32_t r = __builtin_bitreverse32(x);  // field i -> field 15 - i, its bits swapped
-  return ~(((r >> 1) & 0x55555555u) | ((r & 0x55555555u) << 1));
-}
-
-// Eight nibbles in reverse order.
-__device__ __forceinline__ uint32_t rev_nibbles(uint32_t x) {
-  const uint32_t b = __builtin_bswap32(x);
-  return ((b >> 4) & 0x0F0F0F0Fu) | ((b << 4) & 0xF0F0F0F0u);
-}
-
 // The exception bits (nibble bit 3) of sixteen nibbles as a 16-bit mask.
 __device__ __forceinline__ uint32_t nib_exc16(uint32_t x0, uint32_t x1) {
   uint32_t e0 = (x0 >> 3) & 0x11111111u, e1 = (x1 >> 3) & 0x11111111u;
@@ -470,14 +457,9 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     }
   } else {
     // the window's intervals (<= kOrf6RowCap, host-planned), rebased once to
-    // the window so that the per-vector math is 32-bit.  Every interval reads
-    // the forward planes: a '+' interval's vector t covers forward bases
-    // A + 16t .. A + 16t + 15 (A: window position 0), a '-' interval's the
-    // bases A - 16t .. A - 16t + 15 read backwards (A: the low end of vector
-    // 0), reverse-complemented in registers.  Row: {code-plane byte offset of
-    // the word holding A (mod 2^32: only positions inside the interval are
-    // read), A & 31 | exception flag << 5 | '-' << 6, window-relative start,
-    // exception-plane byte offset of the word holding A}
+    // the window so that the per-vector math is 32-bit: {byte offset of the
+    // plane word holding window position 0 (mod 2^32: only positions inside
+    // the interval are read), 4 * nibble shift, window-relative start}
     uint4* const row = reinterpret_cast<uint4*>(s_scratch[wave]);
     uint32_t* const cnt = codes;  // 256 counters, then the vector -> interval map
     const uint64_t e0 = a.tile_e0[tile];
@@ -497,16 +479,17 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const uint32_t jj = lane + 64 * h;
-      const bool rev = (rw[h].y & kOrf6RevRow) != 0;
-      const uint64_t A = rev ? rw[h].x - W0 - 15 : rw[h].x + W0;
-      const uint64_t st = rw[h].y & ~(kOrf6ExcRow | kOrf6RevRow);
+      const uint64_t A = rw[h].x + W0;  // unified base of window position 0
+      const uint64_t st = rw[h].y & ~kOrf6ExcRow;
       const int64_t rs = (int64_t)(st - W0);
       rel[h] = (int32_t)max(min(rs, (int64_t)(1 << 30)), -(int64_t)(1 << 30));
       in[h] = jj <= kOrf6RowCap && st < WE;
+      // {code-plane byte offset of the word holding window position 0,
+      //  A & 31 | exception flag << 5, window-relative start,
+      //  exception-plane byte offset of the word holding window position 0}
       if (jj <= kOrf6RowCap)
         row[jj] = make_uint4((uint32_t)(A >> 4) << 2,
-                             (uint32_t)(A & 31u) | ((rw[h].y & kOrf6ExcRow) ? 32u : 0u) |
-                                 (rev ? 64u : 0u),
+                             (uint32_t)(A & 31u) | ((rw[h].y & kOrf6ExcRow) ? 32u : 0u),
                              (uint32_t)rel[h], (uint32_t)(A >> 5) << 2);
     }
     reinterpret_cast<uint4*>(cnt)[lane] = make_uint4(0u, 0u, 0u, 0u);
@@ -565,21 +548,17 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
         const int32_t t16 = 16 * (int32_t)t;
         const uint4 r0 = row[iv[k]], r1 = row[iv[k] + 1];
         const bool cross = (int32_t)r1.z < min(t16 + 16, wlen);
-        // vector t's word: ascending for '+', descending for '-'
-        const uint32_t da = (r0.y & 64u) ? 0u - 4u * t : 4u * t;
-        const uint32_t db = (r1.y & 64u) ? 0u - 4u * t : 4u * t;
-        const auto va = __builtin_amdgcn_raw_buffer_load_b64(plane2, r0.x + da, 0, 0);
+        const auto va = __builtin_amdgcn_raw_buffer_load_b64(plane2, r0.x + 4u * t, 0, 0);
         const auto vb =
-            __builtin_amdgcn_raw_buffer_load_b64(plane2, cross ? r1.x + db : 0xFFFFFFF0u, 0, 0);
+            __builtin_amdgcn_raw_buffer_load_b64(plane2, cross ? r1.x + 4u * t : 0xFFFFFFF0u, 0, 0);
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
           wa[k][d] = va[d];
           wb[k][d] = vb[d];
         }
         if constexpr (kExc) {
-          const int32_t ta = (r0.y & 64u) ? -t16 : t16, tb = (r1.y & 64u) ? -t16 : t16;
-          const uint32_t ea = r0.w + 4u * (uint32_t)(((int32_t)(r0.y & 31u) + ta) >> 5);
-          const uint32_t eb = r1.w + 4u * (uint32_t)(((int32_t)(r1.y & 31u) + tb) >> 5);
+          const uint32_t ea = r0.w + 4u * (((r0.y & 31u) + 16u * t) >> 5);
+          const uint32_t eb = r1.w + 4u * (((r1.y & 31u) + 16u * t) >> 5);
           const auto ua =
               __builtin_amdgcn_raw_buffer_load_b64(plane1, (r0.y & 32u) ? ea : 0xFFFFFFF0u, 0, 0);
           const auto ub = __builtin_amdgcn_raw_buffer_load_b64(
@@ -608,22 +587,16 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
       const uint32_t j0 = cross ? (uint32_t)((int32_t)r1.z - t16) : 32u;
       const uint32_t mb = j0 >= 16 ? 0u : ~0u << (2 * j0);
       const uint32_t sa = 2u * (r0.y & 15u), sb = 2u * (r1.y & 15u);
-      const bool ra = (r0.y & 64u) != 0, rb = (r1.y & 64u) != 0;
-      const uint32_t fa = funnel4(wa[k][1], wa[k][0], sa);
-      const uint32_t fb = funnel4(wb[k][1], wb[k][0], sb);
-      const uint32_t x0 = ra ? rc_codes(fa) : fa;
-      const uint32_t b0 = rb ? rc_codes(fb) : fb;
+      const uint32_t x0 = funnel4(wa[k][1], wa[k][0], sa);
+      const uint32_t b0 = funnel4(wb[k][1], wb[k][0], sb);
       const uint32_t y0 = (b0 & mb) | (x0 & ~mb);  // codes of positions 0..15
       if (cross && (int32_t)row[iv[k] + 2].z < et) exact |= 1u << k;
       // exception bits of positions 0..15: bit j set = base j not ACGTacgt
       uint32_t ex = 0;
       if (wexc) {
         const uint32_t ma = j0 >= 32 ? 0u : ~0u << j0;
-        const uint32_t ga = funnel4(xa[k][1], xa[k][0], ((r0.y & 31u) + (ra ? 0u - 16u * t : 16u * t)) & 31u);
-        const uint32_t gb = funnel4(xb[k][1], xb[k][0], ((r1.y & 31u) + (rb ? 0u - 16u * t : 16u * t)) & 31u);
-        // bits of a '-' window read backwards: bit j = base 15 - j
-        const uint32_t va = ra ? __builtin_bitreverse32(ga) >> 16 : ga;
-        const uint32_t vb = rb ? __builtin_bitreverse32(gb) >> 16 : gb;
+        const uint32_t va = funnel4(xa[k][1], xa[k][0], ((r0.y & 31u) + 16u * t) & 31u);
+        const uint32_t vb = funnel4(xb[k][1], xb[k][0], ((r1.y & 31u) + 16u * t) & 31u);
         ex = (vb & ma) | (va & ~ma);
       }
       codes[t] = y0;
@@ -648,17 +621,11 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
         while (pos < et) {
           const uint4 r = row[i];
           const int32_t nxt = min((int32_t)row[i + 1].z, et);
-          // nibble-plane byte offset of the word holding A, then vector t's
-          // (ascending for '+', descending for '-': 16 forward bases read
-          // backwards, nibbles reversed and codes complemented)
+          // nibble-plane byte offset of the word holding window position 0
           const uint32_t nboff = 2u * r.x + 4u * ((r.y >> 3) & 1u);
           const uint32_t sh = 4u * (r.y & 7u);
-          const bool rv = (r.y & 64u) != 0;
-          const auto w =
-              __builtin_amdgcn_raw_buffer_load_b96(plane, nboff + (rv ? 0u - 8u * t : 8u * t), 0, 0);
-          const uint32_t f0 = funnel4(w[1], w[0], sh), f1 = funnel4(w[2], w[1], sh);
-          const uint32_t c[2] = {rv ? rev_nibbles(f1) ^ 0x33333333u : f0,
-                                 rv ? rev_nibbles(f0) ^ 0x33333333u : f1};
+          const auto w = __builtin_amdgcn_raw_buffer_load_b96(plane, nboff + 8u * t, 0, 0);
+          const uint32_t c[2] = {funnel4(w[1], w[0], sh), funnel4(w[2], w[1], sh)};
           const int32_t j = pos - t16, n = nxt - pos;
 #pragma unroll
           for (int q = 0; q < 2; ++q) {

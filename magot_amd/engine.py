@@ -35,7 +35,7 @@ class DeviceGenome(object):
     """A GenomeSequence packed into HBM (magot_genome_load).
 
     ``contigs`` is a list of (name, sequence) pairs; sequences are ``str``
-    (latin-1, one char per byte) or ``bytes``.
+    (latin-1, one char per byte), ``bytes`` or uint8 numpy arrays.
     """
 
     def __init__(self, contigs, ctx=None, pack='device'):
@@ -48,7 +48,10 @@ class DeviceGenome(object):
         bufs = []
         for name, seq in contigs:
             names.append(name)
-            bufs.append(np.frombuffer(_as_bytes(seq), dtype=np.uint8))
+            if isinstance(seq, np.ndarray):  # a uint8 view (no copy)
+                bufs.append(np.ascontiguousarray(seq).view(np.uint8).reshape(-1))
+            else:
+                bufs.append(np.frombuffer(_as_bytes(seq), dtype=np.uint8))
         n = len(bufs)
         self.names = names
         self.index = {nm: i for i, nm in enumerate(names)}

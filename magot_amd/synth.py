@@ -61,6 +61,10 @@ class Workload(object):
         return [(self.contig_names[i], self.contig_bytes(i).tobytes())
                 for i in range(len(self.contig_len))]
 
+    def contig_views(self):
+        """(name, uint8 view) per contig: the genome without a copy."""
+        return [(self.contig_names[i], self.contig_bytes(i)) for i in range(len(self.contig_len))]
+
     # -- device plan tables (what the Python walker produces) -----------------
     def plan_tables(self, tx_subset=None):
         """(exons EXON_DTYPE, txs TX_DTYPE) in output order: '+' records

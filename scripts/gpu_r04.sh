@@ -22,6 +22,13 @@ for step in "$@"; do
     slow) timeout -k 10 1100 python -u -m pytest tests -m "gpu and slow" -v -x --timeout 600 --timeout-method thread > $OUT/slow.log 2>&1 || { tail -60 $OUT/slow.log; exit 1; }; tail -3 $OUT/slow.log ;;
     ab5) bash scripts/ab_bench.sh scripts/lib_base.so magot_amd/libmagot.so --config C5 --steps 100 --no-box-state > $OUT/ab5.log 2>&1 || { tail -20 $OUT/ab5.log; exit 1; }; cp -r gpurun_out/ab $OUT/ab5; cat $OUT/ab5.log ;;
     ab3) bash scripts/ab_bench.sh scripts/lib_base.so magot_amd/libmagot.so --steps 300 --no-box-state > $OUT/ab3.log 2>&1 || { tail -20 $OUT/ab3.log; exit 1; }; cp -r gpurun_out/ab $OUT/ab3; cat $OUT/ab3.log ;;
+    probe5) timeout -k 10 600 python scripts/c5_state_probe.py > $OUT/c5_state.json 2> $OUT/c5_state.err || { tail -20 $OUT/c5_state.err; exit 1; }; cat $OUT/c5_state.err | grep '^{' ;;
+    gloo2c5) MAGOT_DIST_BACKEND=gloo timeout -k 10 900 python bench.py --gpus 2 --config C5 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo2_c5.json 2> $OUT/gloo2_c5.err || { tail -30 $OUT/gloo2_c5.err; exit 1; }; grep '^{' $OUT/bench_gloo2_c5.json | cut -c1-600 ;;
+    gloo8c5) MAGOT_DIST_BACKEND=gloo timeout -k 10 1000 python bench.py --gpus 8 --config C5 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo8_c5.json 2> $OUT/gloo8_c5.err || { tail -30 $OUT/gloo8_c5.err; exit 1; }; grep '^{' $OUT/bench_gloo8_c5.json | cut -c1-600 ;;
+    gloo8c3) MAGOT_DIST_BACKEND=gloo timeout -k 10 900 python bench.py --gpus 8 --steps 50 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo8_c3.json 2> $OUT/gloo8_c3.err || { tail -30 $OUT/gloo8_c3.err; exit 1; }; grep '^{' $OUT/bench_gloo8_c3.json | cut -c1-600 ;;
+    packtime) MAGOT_GENOME_TIMING=1 timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify > $OUT/bench_packtime.json 2> $OUT/packtime.err || { tail -30 $OUT/packtime.err; exit 1; }; grep '^\[genome\]' $OUT/packtime.err ;;
+    kt3) rm -rf $OUT/kt3; timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt3 -o kt -- python bench.py --no-box-state > $OUT/kt3.json 2> $OUT/kt3.err || { tail -30 $OUT/kt3.err; exit 1; }; python scripts/rocprof_summary.py --timed C3=$OUT/kt3/kt_kernel_trace.csv,$OUT/kt3.json | head -30 ;;
+    kt5) rm -rf $OUT/kt5; timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt5 -o kt -- python bench.py --config C5 --no-cpu-baseline --no-box-state > $OUT/kt5.json 2> $OUT/kt5.err || { tail -30 $OUT/kt5.err; exit 1; }; python scripts/rocprof_summary.py --timed C5=$OUT/kt5/kt_kernel_trace.csv,$OUT/kt5.json | head -30 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

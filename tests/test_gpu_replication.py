@@ -34,10 +34,17 @@ def _arena(g):
 
 def _defined(g, arena):
     """The arena bytes the layout defines: both nibble planes + 16 bytes of
-    slack, then the runs and the directory (Carve padding excluded)."""
+    slack, the runs (with their sentinel) and the directory -- not the
+    256-byte alignment padding between the pieces, which nothing writes."""
     (o0, l0), (o1, l1) = g.wire_ranges()
     assert o0 == 0
-    return np.concatenate([arena[o0:o0 + 2 * l0 + 16], arena[o1:o1 + l1]])
+    runs = (g.n_exception_runs + 1) * 16
+    o_dir = o1 + ((runs + 255) & ~255)
+    extent = 64 + g.total_bases
+    dir_bytes = 4 * (((extent + 64 + 4095) >> 12) + 2)
+    assert o_dir + dir_bytes <= o1 + l1
+    return np.concatenate([arena[o0:o0 + 2 * l0 + 16], arena[o1:o1 + runs],
+                           arena[o_dir:o_dir + dir_bytes]])
 
 
 def _assert_same_pack(contigs):
@@ -91,9 +98,9 @@ def test_device_pack_edge_genomes(shape):
 
 
 def test_device_pack_crosses_staging_chunks():
-    """A 200 Mb genome: runs cross the 64 MiB pinned staging chunks."""
+    """A 210 Mb genome: runs cross the 64 MiB pinned staging chunks."""
     rng = np.random.default_rng(9)
-    G = 200_000_000
+    G = 210_000_000
     g = np.frombuffer(b'ACGT', np.uint8)[rng.integers(0, 4, size=G, dtype=np.uint8)]
     for c in range(1, 4):  # an N run straddling each chunk boundary
         p = c * (64 << 20)
