@@ -165,6 +165,10 @@ class Gather(object):
             if rank == 0 else None
         self.recv = [self.recv_all[r * cap:(r + 1) * cap] for r in range(world)] \
             if rank == 0 else None
+        # the zero fill runs on torch's stream; the library fills `send` on its
+        # own non-blocking stream, which does not wait for it
+        if str(device).startswith('cuda'):
+            torch.cuda.synchronize()
 
     def run(self):
         src = self.send

@@ -29,6 +29,18 @@ for step in "$@"; do
     packtime) MAGOT_GENOME_TIMING=1 timeout -k 10 600 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify > $OUT/bench_packtime.json 2> $OUT/packtime.err || { tail -30 $OUT/packtime.err; exit 1; }; grep '^\[genome\]' $OUT/packtime.err ;;
     kt3) rm -rf $OUT/kt3; timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt3 -o kt -- python bench.py --no-box-state > $OUT/kt3.json 2> $OUT/kt3.err || { tail -30 $OUT/kt3.err; exit 1; }; python scripts/rocprof_summary.py --timed C3=$OUT/kt3/kt_kernel_trace.csv,$OUT/kt3.json | head -30 ;;
     kt5) rm -rf $OUT/kt5; timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt5 -o kt -- python bench.py --config C5 --no-cpu-baseline --no-box-state > $OUT/kt5.json 2> $OUT/kt5.err || { tail -30 $OUT/kt5.err; exit 1; }; python scripts/rocprof_summary.py --timed C5=$OUT/kt5/kt_kernel_trace.csv,$OUT/kt5.json | head -30 ;;
+    state5)
+      # C5 processes back to back: plain lines (box_state probes) and lines under
+      # UTCL1 translation counters (+ kernel trace), to tell the fast and the slow
+      # state apart by address translation
+      mkdir -p $OUT/state
+      for i in 1 2 3 4; do
+        timeout -k 10 300 python bench.py --config C5 --steps 50 --warmup 5 --no-verify --no-cpu-baseline > $OUT/state/plain$i.json 2> $OUT/state/plain$i.err || { tail -20 $OUT/state/plain$i.err; exit 1; }
+        python3 -c "import json;d=json.load(open('$OUT/state/plain$i.json'));b=d['box_state'];print('plain$i', round(d['roofline']['kernel_ms'],4), b['probe_before'], b['probe_after'])"
+        rm -rf $OUT/state/pmc$i
+        timeout -s KILL 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_STALL_MULTI_MISS_sum --kernel-trace --output-format csv -d $OUT/state/pmc$i -o pmc -- python bench.py --config C5 --steps 30 --warmup 5 --no-verify --no-cpu-baseline --no-box-state > $OUT/state/pmc$i.json 2> $OUT/state/pmc$i.err || { tail -20 $OUT/state/pmc$i.err; exit 1; }
+        python3 -c "import json;d=json.load(open('$OUT/state/pmc$i.json'));print('pmc$i', round(d['roofline']['kernel_ms'],4))"
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

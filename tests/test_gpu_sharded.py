@@ -78,6 +78,7 @@ def _rank_major(parts, sizes):
     """The rank-major receive buffer of a gather (16-byte aligned slots)."""
     cap = (max(max(sizes), 1) + 15) & ~15
     buf = torch.zeros(len(parts) * cap, dtype=torch.uint8, device='cuda')
+    torch.cuda.synchronize()  # the library's stream does not wait for torch's fill
     for r, fill in enumerate(parts):
         if sizes[r]:
             fill(buf[r * cap:].data_ptr())
