@@ -6,7 +6,11 @@ arena) several times, each after a different-size spacer allocation, and
 times 50 back-to-back launches of each (HIP events on the kernel's stream),
 twice round.  The memory probe (torch fill / copy bandwidth) runs beside.
 
-    python scripts/c5_state_probe.py > gpurun_out/c5_state.json
+    python scripts/c5_state_probe.py [--no-probe] [--rounds N] [--spacers 0,64,...]
+        > gpurun_out/c5_state.json
+
+--no-probe skips the memory probe before the first six-frame plan (bench.py
+runs its probe after the plan exists).
 """
 import json
 import os
@@ -18,7 +22,14 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    import argparse
+
     import torch
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--no-probe', action='store_true')
+    ap.add_argument('--rounds', type=int, default=2)
+    ap.add_argument('--spacers', default='0,64,1000,2050,4100,333,0')
+    args = ap.parse_args()
 
     import bench
     from magot_amd import _lib, engine, synth
@@ -27,10 +38,10 @@ def main():
     dev = engine.DeviceGenome(w.contig_views(), ctx=ctx)
     ex, tx = w.plan_tables()
     plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
-    res = {'probe0': bench.memory_probe(), 'runs': []}
-    spacers = [0, 64, 1000, 2050, 4100, 333, 0]  # MiB
+    res = {'probe0': None if args.no_probe else bench.memory_probe(), 'runs': []}
+    spacers = [int(x) for x in args.spacers.split(',')]  # MiB
     keep = []
-    for rnd in range(2):
+    for rnd in range(args.rounds):
         for mib in spacers:
             pad = torch.empty(max(mib, 1) << 20, dtype=torch.uint8, device='cuda')
             o6 = engine.Orf6Plan(plan)

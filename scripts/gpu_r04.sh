@@ -41,6 +41,16 @@ for step in "$@"; do
         timeout -s KILL 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_STALL_MULTI_MISS_sum --kernel-trace --output-format csv -d $OUT/state/pmc$i -o pmc -- python bench.py --config C5 --steps 30 --warmup 5 --no-verify --no-cpu-baseline --no-box-state > $OUT/state/pmc$i.json 2> $OUT/state/pmc$i.err || { tail -20 $OUT/state/pmc$i.err; exit 1; }
         python3 -c "import json;d=json.load(open('$OUT/state/pmc$i.json'));print('pmc$i', round(d['roofline']['kernel_ms'],4))"
       done ;;
+    probeab)
+      # does the memory probe before the six-frame plan decide C5's state?
+      mkdir -p $OUT/probeab
+      for i in 1 2 3; do
+        for v in noprobe probe; do
+          flag=""; [ $v = noprobe ] && flag="--no-probe"
+          timeout -k 10 300 python scripts/c5_state_probe.py $flag --rounds 1 --spacers 0,0 > $OUT/probeab/$v$i.json 2> $OUT/probeab/$v$i.err || { tail -20 $OUT/probeab/$v$i.err; exit 1; }
+          echo "$v$i $(grep '^{' $OUT/probeab/$v$i.err | tr '\n' ' ' | cut -c1-300)"
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
