@@ -703,18 +703,18 @@ def gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx):
     import torch
 
     from magot_amd import engine, shard
-    items = []  # (name, bytes, copy to device address, record offsets)
+    items = []  # (name, bytes, copy to device address, record (starts, lengths))
     if o6 is not None:
-        soff, _ = o6.fetch_to(None)
+        soff, slen = o6.fetch_to(None)
         items.append(('six-frame residues', o6.total, o6.copy_outputs,
-                      np.append(soff[0:-1:6], soff[-1]).astype(np.int64)))
+                      shard.six_frame_blocks(soff, slen)))
     else:
         _, noff, _, poff = plan.fetch()
         items.append(('nucleotides', plan.nuc_bytes,
-                      lambda a: plan.copy_outputs(a, None), noff.astype(np.int64)))
+                      lambda a: plan.copy_outputs(a, None), shard.places(noff)))
         if plan.outputs & engine.OUT_PEP:
             items.append(('peptides', plan.pep_bytes,
-                          lambda a: plan.copy_outputs(None, a), poff.astype(np.int64)))
+                          lambda a: plan.copy_outputs(None, a), shard.places(poff)))
     gathers = [shard.Gather(dist, rank, world, nb) for _, nb, _, _ in items]
     for g, (_, nb, copy, _) in zip(gathers, items):
         if nb:
@@ -726,7 +726,11 @@ def gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx):
         g.run()
     torch.cuda.synchronize()
     t_gather = allreduce_max(dist, time.perf_counter() - t0)
-    offs = [shard.gather_offsets(dist, rank, world, off) for _, _, _, off in items]
+    offs = []
+    for _, _, _, (st, ln) in items:
+        g_st = shard.gather_offsets(dist, rank, world, st)
+        g_ln = shard.gather_offsets(dist, rank, world, ln)
+        offs.append(list(zip(g_st, g_ln)) if rank == 0 else None)
     res = {'seconds': t_gather, 'bytes': int(allreduce_sum(dist, float(sum(it[1] for it in items)))),
            'backend': dist.get_backend(), 'outputs': [it[0] for it in items]}
     if rank != 0:
@@ -746,7 +750,7 @@ def gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx):
         ok = not st.any()
         if o6 is not None:
             out, goff = glob[0]
-            soff, slen = engine.orf6_sizes(roff)
+            soff, slen = engine.orf6_sizes(roff)  # the single-GPU record-order layout
             ok = ok and np.array_equal(goff, soff[0::6].astype(np.int64))
             if ok:
                 bad, first = cds_oracle.orf6_compare(ref, roff, out.cpu().numpy(), soff, slen,

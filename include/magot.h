@@ -345,7 +345,13 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
 /* The same over an extraction plan's records, in HBM (BASELINE configs[4],
  * C5): one kernel gathers each record from the packed genome through the
  * plan's intervals and writes its six translations (the plan's nucleotide
- * output is not needed). */
+ * output is not needed).  The kernel walks the records in genome order and
+ * lays their six-stream blocks out in that order (its stores then stream
+ * through the output): stream j is at the stream_off[j] magot_orf6_fetch
+ * returns (16-byte aligned, stream_len[j] residues, zero padding), a record's
+ * six streams form one contiguous block in the same strand-major order as
+ * magot_orf6_sizes, and stream_off[6n] is the total.  MAGOT_ORF6_ORDER=record
+ * keeps record order (then stream_off equals magot_orf6_sizes'). */
 typedef struct magot_orf6 magot_orf6;
 int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_orf6** out,
                     uint64_t* total_res);

@@ -1504,12 +1504,16 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   rows[2 * ne] = 0;
   rows[2 * ne + 1] = total_nuc;
   starts[ne] = total_nuc;
-  // Processing order.  The kernel walks a concatenation of the records; the
-  // output keeps record order through the per-stream offsets, so the walk may
-  // follow the genome instead: records sorted by the plane position of their
-  // first interval put neighbouring loci into concurrently running tiles (one
-  // XCD sweeps one contiguous range), whose plane reads then share L2 lines.
-  // MAGOT_ORF6_ORDER=record keeps record order.
+  // Processing order.  The kernel walks a concatenation of the records; every
+  // stream is found through its offset, so the walk may follow the genome
+  // instead: records sorted by the plane position of their first interval
+  // put neighbouring loci into concurrently running tiles (one XCD sweeps one
+  // contiguous range), whose plane reads then share L2 lines.  The records'
+  // six-stream blocks are laid out in the same walk order, so each XCD's
+  // stores advance through one contiguous stretch of the output (record
+  // order would scatter them in ~2 KB runs); magot_orf6_fetch returns every
+  // stream's offset.  MAGOT_ORF6_ORDER=record keeps record order (walk and
+  // layout).
   std::vector<uint64_t> noff_k, soff_k;
   uint64_t ne_k = ne;
   {
@@ -1539,7 +1543,6 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
       for (uint64_t k = 0; k < n; ++k) {
         const uint64_t r = perm[k];
         noff_k[k + 1] = noff_k[k] + (noff[r + 1] - noff[r]);
-        for (int s = 0; s < 6; ++s) soff_k[6 * k + s] = o->host_soff[6 * r + s];
         for (uint64_t e = ie[r]; e < ie[r + 1]; ++e) {
           const uint64_t st = starts[e];
           if (starts[e + 1] == st || st >= noff[r + 1]) continue;  // empty
@@ -1556,7 +1559,11 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
           ++j;
         }
       }
-      soff_k[6 * n] = o->host_soff[6 * n];
+      // the blocks in walk order; the fetch table maps record r's streams there
+      if (int rc = magot_orf6_sizes(noff_k.data(), n, soff_k.data(), nullptr, nullptr)) return rc;
+      for (uint64_t k = 0; k < n; ++k)
+        for (int s = 0; s < 6; ++s) o->host_soff[6 * perm[k] + s] = soff_k[6 * k + s];
+      o->host_soff[6 * n] = soff_k[6 * n];
       rows_k[2 * j] = 0;
       rows_k[2 * j + 1] = total_nuc;
       starts_k[j] = total_nuc;

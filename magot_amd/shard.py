@@ -221,24 +221,43 @@ def gather_offsets(dist, rank, world, off):
     return [recv[r][:ns[r]].cpu().numpy() for r in range(world)]
 
 
+def places(off):
+    """(starts, lengths) of the records of an output laid out in record order
+    with prefix offsets ``off`` (records + 1 entries)."""
+    off = np.asarray(off, dtype=np.int64)
+    return off[:-1], off[1:] - off[:-1]
+
+
+def six_frame_blocks(stream_off, stream_len):
+    """(starts, lengths) of every record's block of six 16-byte padded streams
+    in a six-frame output (magot_orf6_fetch: a record's six streams are one
+    contiguous block, wherever the plan placed it)."""
+    soff = np.asarray(stream_off, dtype=np.int64)
+    slen = np.asarray(stream_len, dtype=np.int64).reshape(-1, 6)
+    return soff[0:-1:6], ((slen + 15) & ~15).sum(axis=1)
+
+
 def reassembly_tables(shards, offs, cap):
     """Segment tables that put per-rank outputs back into global record order.
 
-    ``shards[r]``: rank r's global record ids in its output order; ``offs[r]``:
-    its output offsets (records + 1 entries: record j is bytes [offs[r][j],
-    offs[r][j+1]) of its part); ``cap``: the rank stride of the gathered
-    buffer.  Returns (src_off, dst_off, goff) for magot_copy_segments, with
-    goff the global offsets (n+1): dst is laid out in global record order."""
+    ``shards[r]``: rank r's global record ids in its plan's record order;
+    ``offs[r]``: where its records are in its part -- prefix offsets (records
+    + 1 entries: record j is bytes [offs[r][j], offs[r][j+1])) or a (starts,
+    lengths) pair (``places``, ``six_frame_blocks``); ``cap``: the rank stride
+    of the gathered buffer.  Returns (src_off, dst_off, goff) for
+    magot_copy_segments, with goff the global offsets (n+1): dst is laid out
+    in global record order."""
     n_rec = sum(len(sh) for sh in shards)
     lens = np.zeros(n_rec, dtype=np.int64)
     src_off = np.zeros(n_rec, dtype=np.uint64)
     for r, (sh, off) in enumerate(zip(shards, offs)):
-        off = np.asarray(off, dtype=np.int64)
+        st, ln = off if isinstance(off, tuple) else places(off)
+        st = np.asarray(st, dtype=np.int64)
         sh = np.asarray(sh, dtype=np.int64)
-        if len(off) != len(sh) + 1:
-            raise ValueError('rank %d: %d offsets for %d records' % (r, len(off), len(sh)))
-        lens[sh] = off[1:] - off[:-1]
-        src_off[sh] = (r * int(cap) + off[:-1]).astype(np.uint64)
+        if len(st) != len(sh) or len(ln) != len(sh):
+            raise ValueError('rank %d: %d places for %d records' % (r, len(st), len(sh)))
+        lens[sh] = ln
+        src_off[sh] = (r * int(cap) + st).astype(np.uint64)
     goff = np.zeros(n_rec + 1, dtype=np.int64)
     np.cumsum(lens, out=goff[1:])
     return src_off, goff.astype(np.uint64), goff

@@ -51,6 +51,71 @@ for step in "$@"; do
           echo "$v$i $(grep '^{' $OUT/probeab/$v$i.err | tr '\n' ' ' | cut -c1-300)"
         done
       done ;;
+    rehall)
+      # every rank's share of the 2/4/8-GPU C3 job, one at a time on this GPU
+      mkdir -p $OUT/rehearse
+      for kr in 2:0 2:1 4:0 4:1 4:2 4:3 8:0 8:1 8:2 8:3 8:4 8:5 8:6 8:7; do
+        timeout -k 10 300 python bench.py --rehearse-shard $kr --steps 300 --no-cpu-baseline --no-verify --no-box-state > $OUT/rehearse/r_${kr/:/_}.json 2> $OUT/rehearse/r.err || { tail -20 $OUT/rehearse/r.err; exit 1; }
+        python3 -c "import json;d=json.load(open('$OUT/rehearse/r_${kr/:/_}.json'));r=d['roofline'];print('$kr', round(d['ms_per_step'],5), round(r['kernel_ms'],5), d['config']['cds_bases_rank0'], d['config']['exons_rank0'])"
+      done ;;
+    half)
+      # why is half of C3 more than half the time?  tile sizes / caps on the 2:0 share
+      mkdir -p $OUT/half
+      for rep in 1 2; do
+        for v in full:5 2_0:5 2_0:3 2_0:4 full:3 2_0:5:bpc5 2_0:5:bpc7; do
+          IFS=: read what lc extra <<< "$v"
+          args="--steps 300 --no-cpu-baseline --no-verify --no-box-state"
+          [ $what = 2_0 ] && args="$args --rehearse-shard 2:0"
+          envs="MAGOT_EXTRACT_LANE_CHUNKS=$lc"
+          [ "$extra" = bpc5 ] && envs="$envs MAGOT_EXTRACT_BLOCKS_PER_CU=5"
+          [ "$extra" = bpc7 ] && envs="$envs MAGOT_EXTRACT_BLOCKS_PER_CU=7"
+          env $envs timeout -k 10 300 python bench.py $args > $OUT/half/$v.$rep.json 2> $OUT/half/err || { tail -20 $OUT/half/err; exit 1; }
+          python3 -c "import json;d=json.load(open('$OUT/half/$v.$rep.json'));r=d['roofline'];print('$v', round(d['ms_per_step'],5), round(r['kernel_ms'],5))"
+        done
+      done ;;
+    halfpmc)
+      mkdir -p $OUT/halfpmc
+      for what in full 2_0; do
+        args="--steps 20 --warmup 2 --settle-ms 0 --no-cpu-baseline --no-verify --no-box-state"
+        [ $what = 2_0 ] && args="$args --rehearse-shard 2:0"
+        i=0
+        for grp in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CYCLES"; do
+          i=$((i+1))
+          rm -rf $OUT/halfpmc/$what.$i
+          timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/halfpmc/$what.$i -o pmc -- python bench.py $args > $OUT/halfpmc/$what.$i.log 2>&1 || { echo "pmc $what $i failed"; tail -5 $OUT/halfpmc/$what.$i.log; exit 1; }
+        done
+      done
+      python3 scripts/pmc_summary.py $OUT/halfpmc 2>/dev/null | head -5; echo halfpmc done ;;
+    abreh)
+      # AB_B=scripts/lib_X.so: base vs variant on the full C3 job and one GPU's
+      # share of the 2/4/8-GPU job, alternating, two rounds
+      mkdir -p $OUT/abreh
+      for rep in 1 2; do
+        for what in full 2:0 4:0 8:0; do
+          for v in A B; do
+            lib=scripts/lib_base.so; [ $v = B ] && lib=$AB_B
+            args="--steps 300 --no-cpu-baseline --no-verify --no-box-state"
+            [ $what != full ] && args="$args --rehearse-shard $what"
+            MAGOT_LIB=$lib timeout -k 10 300 python bench.py $args > $OUT/abreh/$v.${what/:/_}.$rep.json 2> $OUT/abreh/err || { tail -20 $OUT/abreh/err; exit 1; }
+            python3 -c "import json;d=json.load(open('$OUT/abreh/$v.${what/:/_}.$rep.json'));r=d['roofline'];print('$v $what', round(d['ms_per_step'],5), round(r['kernel_ms'],5))"
+          done
+        done
+      done ;;
+    state2)
+      # write-path probe, C5 line, C5 traffic replay, probe again: does C5's
+      # slow state go with a slow tiled write stream on the same box?
+      mkdir -p $OUT/state2
+      /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 scripts/membench5.hip -o /tmp/membench5.bin || exit 1
+      /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 scripts/solbench.hip -o /tmp/solbench.bin || exit 1
+      MB5_PROBE=1 timeout -k 10 120 /tmp/membench5.bin > $OUT/state2/probe1.txt 2>&1 || exit 1
+      timeout -k 10 300 python bench.py --config C5 --steps 50 --warmup 5 --no-verify --no-cpu-baseline > $OUT/state2/c5.json 2> $OUT/state2/c5.err || { tail -20 $OUT/state2/c5.err; exit 1; }
+      timeout -k 10 300 /tmp/solbench.bin c5 > $OUT/state2/solbench_c5.txt 2>&1 || exit 1
+      MB5_PROBE=1 timeout -k 10 120 /tmp/membench5.bin > $OUT/state2/probe2.txt 2>&1 || exit 1
+      timeout -k 10 300 python bench.py --steps 100 --no-verify --no-cpu-baseline > $OUT/state2/c3.json 2> $OUT/state2/c3.err || { tail -20 $OUT/state2/c3.err; exit 1; }
+      cat $OUT/state2/probe1.txt; python3 -c "import json;d=json.load(open('$OUT/state2/c5.json'));print('C5', round(d['roofline']['kernel_ms'],4), d['box_state']['probe_before'])"
+      grep "scattered, buffer 1\|sequential runs " $OUT/state2/solbench_c5.txt | head -4; cat $OUT/state2/probe2.txt
+      python3 -c "import json;d=json.load(open('$OUT/state2/c3.json'));print('C3', round(d['roofline']['kernel_ms'],5))" ;;
+    orf6check) timeout -k 10 900 $PYT --timeout 400 tests/test_gpu_parity.py -k "orf6 or c5_full" tests/test_gpu_sharded.py::test_c5_shards_reassembled_six_frames_vs_c_oracle > $OUT/orf6check.log 2>&1 || { tail -40 $OUT/orf6check.log; exit 1; }; tail -2 $OUT/orf6check.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -213,7 +213,7 @@ def test_six_frame_blocks_reassemble_to_single_gpu_layout():
                 part[int(soff[6 * i + k]):int(soff[6 * i + k]) + int(slen[6 * i + k])] = \
                     (j * 37 + 11) & 0xFF
         parts.append(part)
-        offs.append(np.append(soff[0:-1:6], soff[-1]).astype(np.int64))
+        offs.append(shard.six_frame_blocks(soff, slen))
     got, goff = shard.reassemble(shards, parts, offs)
     assert np.array_equal(goff, gsoff[0::6].astype(np.int64))
     assert np.array_equal(got, glob)
@@ -229,6 +229,14 @@ def test_reassembly_tables_rank_major():
     assert src.tolist() == [16, 0, 18, 5, 18]
     with pytest.raises(ValueError):
         shard.reassembly_tables(shards, [offs[0], offs[1][:-1]], cap=16)
+    # (starts, lengths) places: rank 1 lays its records out as 4, 0, 2
+    pl = [(np.array([0, 5]), np.array([5, 1])), (np.array([7, 9, 0]), np.array([2, 0, 7]))]
+    src2, dst2, goff2 = shard.reassembly_tables(shards, pl, cap=16)
+    assert dst2.tolist() == goff.tolist() and src2.tolist() == [23, 0, 25, 5, 16]
+    # six-frame blocks: a record's six padded streams
+    st, ln = shard.six_frame_blocks(np.array([32, 48, 64, 96, 112, 128, 0, 0, 0, 0, 0, 16, 144]),
+                                    np.array([10, 16, 20, 1, 0, 16, 0, 0, 0, 0, 0, 3]))
+    assert st.tolist() == [32, 0] and ln.tolist() == [16 + 16 + 32 + 16 + 0 + 16, 16]
 
 
 def _gather_worker(rank, world, port, q):

@@ -135,8 +135,8 @@ def test_c5_shards_reassembled_six_frames_vs_c_oracle(n):
             o6s.append(o)
         offs = []
         for o in o6s:
-            soff, _ = o.fetch_to(None)
-            offs.append(np.append(soff[0:-1:6], soff[-1]).astype(np.int64))
+            soff, slen = o.fetch_to(None)
+            offs.append(shard.six_frame_blocks(soff, slen))  # blocks in the plan's walk order
         buf, cap = _rank_major([o.copy_outputs for o in o6s], [o.total for o in o6s])
         for o in o6s:
             o.close()
