@@ -1404,7 +1404,7 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
   const uint64_t o_in = cv.take<uint8_t>(total + 64);
   const uint64_t o_out = cv.take<uint8_t>(total_res + 64);
   const uint64_t o_off = cv.take<uint64_t>(n + 1);
-  const uint64_t o_soff = cv.take<uint64_t>(6 * n + 1);
+  const uint64_t o_boff = cv.take<uint64_t>(n + 1);
   const uint64_t o_t0 = cv.take<uint64_t>(n_tiles + 1);
   const uint64_t o_r0 = cv.take<uint32_t>(n_tiles);
   const uint64_t o_lut = cv.take<uint8_t>(256);
@@ -1416,9 +1416,12 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
     e = hipMemcpyAsync(base + o_lut, tables, 256, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(base + o_off, seq_off, (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream);
+  // the kernel takes each record's block start (its streams' places follow
+  // from the record length, magot_orf6_sizes' layout)
+  std::vector<uint64_t> boff(n + 1);
+  for (uint64_t r = 0; r <= n; ++r) boff[r] = stream_off[6 * r];
   if (e == hipSuccess)
-    e = hipMemcpyAsync(base + o_soff, stream_off, (6 * n + 1) * 8, hipMemcpyHostToDevice,
-                       ctx->stream);
+    e = hipMemcpyAsync(base + o_boff, boff.data(), (n + 1) * 8, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(base + o_t0, tiles.t0.data(), (n_tiles + 1) * 8, hipMemcpyHostToDevice,
                        ctx->stream);
@@ -1431,7 +1434,7 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
     a.noff = reinterpret_cast<const uint64_t*>(base + o_off);
     a.n_rec = n;
     a.total = total;
-    a.soff = reinterpret_cast<const uint64_t*>(base + o_soff);
+    a.boff = reinterpret_cast<const uint64_t*>(base + o_boff);
     a.tile_t0 = reinterpret_cast<const uint64_t*>(base + o_t0);
     a.tile_r0 = reinterpret_cast<const uint32_t*>(base + o_r0);
     a.n_tiles = n_tiles;
@@ -1586,7 +1589,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   orf6_tables(lut, tables);
   Carve cv;
   const uint64_t o_off = cv.take<uint64_t>(o->n_rec + 1);
-  const uint64_t o_soff = cv.take<uint64_t>(6 * o->n_rec + 1);
+  const uint64_t o_boff = cv.take<uint64_t>(o->n_rec + 1);
   const uint64_t o_out = cv.take<uint8_t>(o->total + 64);
   const uint64_t o_rows = cv.take<uint64_t>(2 * (ne_k + 1));
   const uint64_t o_t0 = cv.take<uint64_t>(n_tiles + 1);
@@ -1611,7 +1614,9 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   MAGOT_HIP_TRY(hipGetLastError());
   MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   MAGOT_HIP_TRY(up(o_off, noff_k.data(), (o->n_rec + 1) * 8));
-  MAGOT_HIP_TRY(up(o_soff, soff_k.data(), (6 * o->n_rec + 1) * 8));
+  std::vector<uint64_t> boff_k(o->n_rec + 1);  // block starts in walk order
+  for (uint64_t k = 0; k <= o->n_rec; ++k) boff_k[k] = soff_k[6 * k];
+  MAGOT_HIP_TRY(up(o_boff, boff_k.data(), (o->n_rec + 1) * 8));
   MAGOT_HIP_TRY(up(o_rows, rows.data(), rows.size() * 8));
   MAGOT_HIP_TRY(up(o_t0, tiles.t0.data(), (n_tiles + 1) * 8));
   MAGOT_HIP_TRY(up(o_r0, tiles.r0.data(), n_tiles * 4));
@@ -1631,7 +1636,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   a.noff = reinterpret_cast<const uint64_t*>(base + o_off);
   a.n_rec = o->n_rec;
   a.total = total_nuc;
-  a.soff = reinterpret_cast<const uint64_t*>(base + o_soff);
+  a.boff = reinterpret_cast<const uint64_t*>(base + o_boff);
   a.tile_t0 = reinterpret_cast<const uint64_t*>(base + o_t0);
   a.tile_r0 = reinterpret_cast<const uint32_t*>(base + o_r0);
   a.tile_e0 = reinterpret_cast<const uint32_t*>(base + o_e0);

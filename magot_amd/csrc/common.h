@@ -236,8 +236,10 @@ void launch_mirror_planes(uint32_t* nib, uint64_t span, hipStream_t s);
 void launch_revcomp(const uint8_t* in, const uint64_t* off, uint64_t n, uint64_t total,
                     uint8_t* out, hipStream_t s);
 // Six translations per record for Sequence.get_orfs (orf6_kernel): stream
-// j = 6*record + 2*frame + (strand == '+'), soff = 6*n_rec+1 padded residue
-// offsets; noff = n_rec+1 offsets of the records in the concatenation.
+// j = 6*record + 2*frame + (strand == '+'); boff = n_rec+1 offsets of each
+// record's block of six 16-byte padded streams (strand-major inside the block,
+// magot_orf6_sizes; the kernel derives each stream's place from the record's
+// length); noff = n_rec+1 offsets of the records in the concatenation.
 // The records are either bytes (nuc, readable up to the next 16-byte
 // boundary) or gathered from the genome plane through interval rows
 // {unified anchor, start} (n_rows + a sentinel row {0, total}): base P of
@@ -259,7 +261,7 @@ struct Orf6Args {
   const uint64_t* noff;
   uint64_t n_rec;
   uint64_t total;
-  const uint64_t* soff;
+  const uint64_t* boff;
   const uint64_t* tile_t0;
   const uint32_t* tile_r0;
   const uint32_t* tile_e0;

@@ -150,9 +150,10 @@ __global__ __launch_bounds__(kOpsThreads) void translate_kernel(
 // trimX removes for frames 1/2); frame 0 keeps its first residue and the
 // caller applies trimX.  Stream j = 6*record + 2*f + (strand == '+').
 //
-// Output layout: every stream starts on a 16-byte boundary (soff holds the
-// padded offsets, the real lengths follow from the record length); the
-// bytes of a stream's last 16-byte chunk past its end are zero.
+// Output layout: a record's six streams are one block at boff[record], its
+// three '-' streams then its three '+' streams, each on a 16-byte boundary
+// (the places and real lengths follow from the record length); the bytes of
+// a stream's last 16-byte chunk past its end are zero.
 //
 // Input-stationary: one wave owns a tile of kOrfTile bases of the
 // concatenated records and every output chunk whose first codon starts in
@@ -396,15 +397,15 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     s_code[threadIdx.x] = (uint8_t)(c < 4 ? c : 0x40u);
     __syncthreads();
   }
-  // XCD-aware tile order: blocks are dealt round-robin to the 8 XCDs, so
-  // virtual block vb gives each XCD one contiguous run of tiles.  A record
-  // cut by a tile boundary leaves a partial 128-byte line in each of its six
-  // streams; with both tiles on one XCD the two halves merge in that XCD's
-  // L2.  Together with plain (not non-temporal) stores here: WRITE_SIZE 5.26
-  // -> 5.06 GB per launch, C5 step 1.72 -> 1.65 ms (A/B, one box, medians).
-  const uint32_t xnb = gridDim.x, xb = blockIdx.x;
-  const uint32_t xq = xnb >> 3, xr = xnb & 7, xcd = xb & 7, xk = xb >> 3;
-  const uint32_t vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  // Tile order = block order, dealt round-robin to the 8 XCDs by the hardware.
+  // Since the record blocks are laid out in walk order (magot_plan_orf6), all
+  // XCDs then advance together through one stretch of the output.  Before that
+  // layout, one contiguous run of tiles per XCD merged the partial lines two
+  // tiles share in one L2 (WRITE_SIZE 5.26 -> 5.06 GB, C5 1.72 -> 1.65 ms); with
+  // it, round-robin is 1 % faster than contiguous runs (1.406 / 1.408 / 1.406 vs
+  // 1.420 / 1.422 / 1.422 ms) and than runs of 16 or 256 blocks (1.416-1.418 ms,
+  // profiles/r04n/).
+  const uint32_t vb = blockIdx.x;
   const uint64_t tile = (uint64_t)vb * (kOpsThreads / 64) + wave;
   if (tile >= a.n_tiles) return;  // wave-uniform
   s_tblw[lane] = reinterpret_cast<const uint32_t*>(a.tables)[lane];
@@ -420,7 +421,6 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
   const uint32_t my_k = (uint32_t)(lane < kOrfSegs / 2 ? lane : lane - kOrfSegs / 2);
   const uint32_t my_rec = my_k / 3u, my_f = my_k % 3u;
   const bool my_plus = lane >= kOrfSegs / 2;
-  const uint32_t my_s = 2u * my_f + (my_plus ? 1u : 0u);
   // the first record batch's offsets, in flight with the staging loads
   // (unconditional clamped loads: a branch here would wait for them before
   // the staging loads are issued)
@@ -707,7 +707,13 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
       const int64_t p = my_plus ? (int64_t)(nb + 2 * my_f + 48 * lo)
                                 : (int64_t)(nb + L - 3 - 2 * my_f - 48 * lo);
       OrfSeg g;
-      g.out0 = a.soff[6 * r + my_s] + 16 * lo - 16 * (uint64_t)start;
+      // the stream's place in the record's block (magot_orf6_sizes): strand-
+      // major, each of the three frames padded to 16 bytes
+      const uint64_t p0 = (orf_count(L, 0) + 15) & ~15ull, p1 = (orf_count(L, 1) + 15) & ~15ull;
+      const uint64_t p2 = (orf_count(L, 2) + 15) & ~15ull;
+      const uint64_t within = (my_plus ? p0 + p1 + p2 : 0) + (my_f >= 1 ? p0 : 0) +
+                              (my_f >= 2 ? p1 : 0);
+      g.out0 = a.boff[r] + within + 16 * lo - 16 * (uint64_t)start;
       g.p0 = (int32_t)(p - (int64_t)W0 + (my_plus ? -48 : 48) * (int64_t)start);
       const int32_t rem = (int32_t)(nres - 16 * lo) + 16 * (int32_t)start;
       g.rem0 = my_plus ? rem : -rem;

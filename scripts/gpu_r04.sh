@@ -116,6 +116,16 @@ for step in "$@"; do
       grep "scattered, buffer 1\|sequential runs " $OUT/state2/solbench_c5.txt | head -4; cat $OUT/state2/probe2.txt
       python3 -c "import json;d=json.load(open('$OUT/state2/c3.json'));print('C3', round(d['roofline']['kernel_ms'],5))" ;;
     orf6check) timeout -k 10 900 $PYT --timeout 400 tests/test_gpu_parity.py -k "orf6 or c5_full" tests/test_gpu_sharded.py::test_c5_shards_reassembled_six_frames_vs_c_oracle > $OUT/orf6check.log 2>&1 || { tail -40 $OUT/orf6check.log; exit 1; }; tail -2 $OUT/orf6check.log ;;
+    abn)
+      # ABN_LIBS="a.so b.so ..." ABN_ARGS="--config C5": the libraries alternated, 3 rounds
+      mkdir -p $OUT/abn
+      for rep in 1 2 3; do
+        for lib in $ABN_LIBS; do
+          n=$(basename $lib .so)
+          MAGOT_LIB=$lib timeout -k 10 300 python bench.py --no-verify --no-cpu-baseline --no-box-state $ABN_ARGS > $OUT/abn/$n.$rep.json 2> $OUT/abn/err || { tail -20 $OUT/abn/err; exit 1; }
+          python3 -c "import json;d=json.load(open('$OUT/abn/$n.$rep.json'));print('$n', round(d['roofline']['kernel_ms'],5), round(d['ms_per_step'],5))"
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
