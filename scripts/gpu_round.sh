@@ -9,7 +9,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
-# stages: tests slow bench driver c2 c5 multi rehearse kt kt5 kt2 pmc traffic smoke
+# stages: tests slow bench driver c2 c5 multi multi5 rehearse kt kt5 kt2 pmc traffic e2e smoke
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
 bash scripts/box_info.sh $OUT/box_before
@@ -38,6 +38,16 @@ if has c5; then
   timeout -k 10 600 python $BENCH --config C5 > $OUT/bench_c5.json 2> $OUT/c5.err || { tail -30 $OUT/c5.err; exit 1; }
   cat $OUT/bench_c5.json
 fi
+if has multi5; then
+  # the C5 job over two ranks sharing the card (gloo): six-frame outputs gathered back
+  MAGOT_DIST_BACKEND=gloo timeout -k 10 900 python $BENCH --gpus 2 --config C5 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo2_c5.json 2> $OUT/gloo2_c5.err || { tail -30 $OUT/gloo2_c5.err; exit 1; }
+  grep '^{' $OUT/bench_gloo2_c5.json | cut -c1-400
+fi
+if has e2e; then
+  MAGOT_GENOME_TIMING=1 MAGOT_GFF_TIMING=1 timeout -k 10 900 python scripts/e2e_cli.py --config C3 --seq-type protein > $OUT/e2e_protein.json 2> $OUT/e2e.err || { tail -20 $OUT/e2e.err; exit 1; }
+  cat $OUT/e2e_protein.json
+  rm -rf /tmp/magot_e2e
+fi
 if has multi; then
   # two ranks launched by bench itself, sharing the one card over gloo (the
   # C4 orchestration; the driver's 8-GPU node runs it over RCCL)
@@ -45,8 +55,10 @@ if has multi; then
   grep '^{' $OUT/bench_gloo2.json
 fi
 if has kt; then
+  # the bench line under the kernel trace; rocprof_summary.py --timed averages
+  # exactly the line's K timed dispatches (roofline.timed_launches)
   rm -rf $OUT/kt
-  timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python $BENCH > $OUT/kt.json 2> $OUT/kt.err || { tail -30 $OUT/kt.err; exit 1; }
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python $BENCH --no-box-state > $OUT/kt.json 2> $OUT/kt.err || { tail -30 $OUT/kt.err; exit 1; }
   grep -h extract_kernel $OUT/kt/kt_kernel_stats.csv
   cat $OUT/kt.json
 fi
@@ -60,7 +72,7 @@ fi
 for cfg in C5 C2; do
   if has kt${cfg:1}; then
     rm -rf $OUT/kt_$cfg
-    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$cfg -o kt -- python $BENCH --config $cfg --no-cpu-baseline > $OUT/kt_$cfg.json 2> $OUT/kt_$cfg.err || { tail -30 $OUT/kt_$cfg.err; exit 1; }
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt_$cfg -o kt -- python $BENCH --config $cfg --no-cpu-baseline --no-box-state > $OUT/kt_$cfg.json 2> $OUT/kt_$cfg.err || { tail -30 $OUT/kt_$cfg.err; exit 1; }
     grep -h "orf6_kernel\|extract_kernel" $OUT/kt_$cfg/kt_kernel_stats.csv
   fi
 done
@@ -72,7 +84,7 @@ if has pmc; then
              "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
     i=$((i+1))
     rm -rf $OUT/pmc$i
-    timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python bench.py --steps 5 --warmup 1 --no-verify --no-cpu-baseline > $OUT/pmc$i.log 2>&1
+    timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python bench.py --steps 5 --warmup 1 --no-verify --no-cpu-baseline --no-box-state > $OUT/pmc$i.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "pmc group $i failed rc=$rc"; tail -3 $OUT/pmc$i.log; [ $rc -ge 124 ] && exit 1; fi
   done
@@ -85,7 +97,7 @@ if has traffic; then
     c=${cfg%%:*}
     for grp in FETCH_SIZE WRITE_SIZE; do
       rm -rf $OUT/traffic_$c/$grp
-      timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/traffic_$c/$grp -o pmc -- python bench.py --config $c --steps 5 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline > $OUT/traffic_$c.$grp.log 2>&1 || { echo "traffic $c $grp failed"; tail -3 $OUT/traffic_$c.$grp.log; exit 1; }
+      timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/traffic_$c/$grp -o pmc -- python bench.py --config $c --steps 5 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline --no-box-state > $OUT/traffic_$c.$grp.log 2>&1 || { echo "traffic $c $grp failed"; tail -3 $OUT/traffic_$c.$grp.log; exit 1; }
     done
   done
   echo traffic ok
