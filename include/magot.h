@@ -200,13 +200,15 @@ int magot_genome_attach_wire(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_
  * Reassembly of a sharded job's outputs on one device (outputs
  * gathered back, final order restored from the global record index): for
  * i < n, dst[dst_off[i], dst_off[i+1]) = src[src_off[i], src_off[i] +
- * dst_off[i+1] - dst_off[i]).  src and dst are device memory (e.g. the buffer
- * an RCCL gather filled, rank-major), dst_off has n+1 non-decreasing entries,
- * the offset tables are host arrays.  Synchronous.  No reference counterpart
- * (the reference is single-process).
+ * dst_off[i+1] - dst_off[i]).  src (src_bytes long) and dst (dst_off[n] long)
+ * are device memory (e.g. the buffer an RCCL gather filled, rank-major),
+ * dst_off has n+1 non-decreasing entries, the offset tables are host arrays;
+ * a segment reaching past src_bytes is refused (MAGOT_ERR_RANGE) before any
+ * launch.  Synchronous.  No reference counterpart (the reference is
+ * single-process).
  */
-int magot_copy_segments(magot_ctx* ctx, const void* src_dev, void* dst_dev, const uint64_t* src_off,
-                        const uint64_t* dst_off, uint64_t n);
+int magot_copy_segments(magot_ctx* ctx, const void* src_dev, uint64_t src_bytes, void* dst_dev,
+                        const uint64_t* src_off, const uint64_t* dst_off, uint64_t n);
 
 /*
  * Build a device-resident plan: interval table -> output offsets, ~3 KiB

@@ -148,7 +148,8 @@ def _declare(lib):
                                                     ctypes.POINTER(ctypes.c_uint32)]),
         'magot_genome_attach_wire': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp,
                                                     ctypes.POINTER(_vp)]),
-        'magot_copy_segments': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, ctypes.c_uint64]),
+        'magot_copy_segments': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
+                                               ctypes.c_uint64]),
         'magot_ctx_mark': (ctypes.c_int, [_vp, ctypes.c_int]),
         'magot_orf6_copy_outputs': (ctypes.c_int, [_vp, _vp, _vp]),
         'magot_ctx_elapsed': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double)]),

@@ -709,8 +709,8 @@ int magot_genome_attach_wire(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_
   return MAGOT_OK;
 }
 
-int magot_copy_segments(magot_ctx* ctx, const void* src_dev, void* dst_dev, const uint64_t* src_off,
-                        const uint64_t* dst_off, uint64_t n) {
+int magot_copy_segments(magot_ctx* ctx, const void* src_dev, uint64_t src_bytes, void* dst_dev,
+                        const uint64_t* src_off, const uint64_t* dst_off, uint64_t n) {
   if (int rc = bind(ctx)) return rc;
   if (!src_off || !dst_off) {
     set_error("magot_copy_segments: null argument");
@@ -721,11 +721,17 @@ int magot_copy_segments(magot_ctx* ctx, const void* src_dev, void* dst_dev, cons
     set_error("magot_copy_segments: null buffer");
     return MAGOT_ERR_ARG;
   }
-  for (uint64_t i = 0; i < n; ++i)
+  for (uint64_t i = 0; i < n; ++i) {
     if (dst_off[i + 1] < dst_off[i]) {
       set_error("magot_copy_segments: dst_off must be non-decreasing");
       return MAGOT_ERR_ARG;
     }
+    const uint64_t len = dst_off[i + 1] - dst_off[i];
+    if (len && (src_off[i] > src_bytes || len > src_bytes - src_off[i])) {
+      set_error("magot_copy_segments: segment " + std::to_string(i) + " reads past src_bytes");
+      return MAGOT_ERR_RANGE;
+    }
+  }
   DevBuf tables;
   MAGOT_HIP_TRY(hipMalloc(&tables.p, (2 * n + 1) * 8));
   uint64_t* d_src = static_cast<uint64_t*>(tables.p);

@@ -686,15 +686,16 @@ class Orf6Plan(object):
             pass
 
 
-def copy_segments(src_dev_ptr, dst_dev_ptr, src_off, dst_off, ctx=None):
+def copy_segments(src_dev_ptr, src_bytes, dst_dev_ptr, src_off, dst_off, ctx=None):
     """dst[dst_off[i]:dst_off[i+1]] = src[src_off[i]:...] on the device
-    (magot_copy_segments; addresses of device memory, host offset tables)."""
+    (magot_copy_segments; addresses of device memory, src_bytes the source's
+    size, host offset tables)."""
     ctx = ctx or _lib.default_context()
     so = np.ascontiguousarray(src_off, dtype=np.uint64)
     do = np.ascontiguousarray(dst_off, dtype=np.uint64)
     if len(do) != len(so) + 1:
         raise ValueError('dst_off needs len(src_off) + 1 entries')
-    check(_lib.lib().magot_copy_segments(ctx.handle, ctypes.c_void_p(src_dev_ptr),
+    check(_lib.lib().magot_copy_segments(ctx.handle, ctypes.c_void_p(src_dev_ptr), int(src_bytes),
                                          ctypes.c_void_p(dst_dev_ptr), ptr(so), ptr(do), len(so)),
           'magot_copy_segments')
 

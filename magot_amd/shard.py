@@ -273,7 +273,8 @@ def reassemble_device(shards, offs, gathered, cap, ctx=None):
     src_off, dst_off, goff = reassembly_tables(shards, offs, cap)
     out = torch.empty(max(int(goff[-1]), 1), dtype=torch.uint8, device=gathered.device)
     torch.cuda.synchronize()
-    engine.copy_segments(gathered.data_ptr(), out.data_ptr(), src_off, dst_off, ctx=ctx)
+    engine.copy_segments(gathered.data_ptr(), gathered.numel(), out.data_ptr(), src_off, dst_off,
+                         ctx=ctx)
     return out[:int(goff[-1])], goff
 
 

@@ -212,7 +212,13 @@ def test_copy_segments_vs_numpy(aligned):
     d_src = torch.from_numpy(src).cuda()
     d_dst = torch.full((int(dst_off[-1]) + 64,), 0xEE, dtype=torch.uint8, device='cuda')
     torch.cuda.synchronize()
-    engine.copy_segments(d_src.data_ptr(), d_dst.data_ptr(), src_off, dst_off)
+    engine.copy_segments(d_src.data_ptr(), src_bytes, d_dst.data_ptr(), src_off, dst_off)
     got = d_dst.cpu().numpy()
     assert np.array_equal(got[:int(dst_off[-1])], want)
     assert (got[int(dst_off[-1]):] == 0xEE).all()  # nothing written past the end
+    # a segment reaching past the source is refused before any launch
+    bad = src_off.copy()
+    i = int(np.argmax(lens))
+    bad[i] = src_bytes - int(lens[i]) + 1
+    with pytest.raises(engine.MagotError):
+        engine.copy_segments(d_src.data_ptr(), src_bytes, d_dst.data_ptr(), bad, dst_off)
