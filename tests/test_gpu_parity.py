@@ -557,6 +557,18 @@ def test_orf6_over_extraction_plan_vs_oracle(monkeypatch, walk):
     o6 = engine.Orf6Plan(plan)
     o6.execute()
     out, soff, slen = o6.fetch()
+    # the plan's layout: each record's six streams one 16-byte aligned block,
+    # the blocks tiling [0, total) (in walk order by default, record order
+    # under MAGOT_ORF6_ORDER=record)
+    from magot_amd import shard
+    st, ln = shard.six_frame_blocks(soff, slen)
+    order = np.argsort(st, kind='stable')
+    assert (st % 16 == 0).all() and int(soff[-1]) == o6.total
+    assert np.array_equal(np.cumsum(ln[order])[:-1], st[order][1:]) and st[order][0] == 0
+    assert int(st[order][-1] + ln[order][-1]) == o6.total
+    if walk == 'record':
+        ref_soff, _ = engine.orf6_sizes(noff)
+        assert np.array_equal(soff, ref_soff)
     raw = out.tobytes().decode('latin-1')
     for r in range(len(tx)):
         s = nuc[int(noff[r]):int(noff[r + 1])].tobytes().decode('latin-1')
