@@ -1494,7 +1494,7 @@ int magot_plan_orf6(magot_ctx* ctx, magot_plan* p, const uint8_t* lut64, magot_o
   // interval rows {unified anchor, start} from the plan's compacted table
   // (a '-' interval reads the mirror plane forward; staging every interval
   // from the forward planes instead, '-' read backwards and reverse-
-  // complemented in registers, measured 5 % slower: DESIGN.md 3, round 4)
+  // complemented in registers, measured 5 % slower: DESIGN.md 4, round 4)
   const uint64_t ne = p->n_ex_c;
   std::vector<uint64_t> ex_g(ne), ex_out(ne + 1), rows(2 * (ne + 1));
   if (ne) {

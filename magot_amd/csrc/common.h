@@ -109,7 +109,7 @@ constexpr int kChunk = 16;                    // bytes per lane-store
 // (3024-byte tiles) for translating plans too small to fill the chip several
 // times over (one GPU's share of an 8-GPU C4 job: -3.5 % per launch; 4-GPU
 // share -2.7 %; but the 2-GPU share +8 %, C2 (nucleotides only) +5.5 %, and at
-// full C3 size 4 slots are +3.6 % slower; A/Bs in DESIGN.md).
+// full C3 size 4 slots are +3.6 % slower; A/Bs in EXPERIMENTS.md §3).
 constexpr int kLaneChunksLarge = 5, kLaneChunksSmall = 3;
 // Output bytes of a tile cut for `lane_chunks` slots per lane (3 slots of halo):
 // 5072 for the large tile (<= 1691 residues, <= 106 residue chunks), 3024 for

@@ -6,7 +6,7 @@ It exists to CHECK the MI355X product (``magot_amd``); it is never imported by
 the product.  Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
 ``cpu_baseline`` leg may use it.
 
-Pinning (see DESIGN.md "Oracle"):
+Pinning ("Oracle and parity"):
   * ``test_data/test_suite.py:12,13,14`` cksums reproduced on the C14 genome
     rebuilt from the reference's own fixtures (``tests/golden/c14.py``);
   * O.biroi outputs captured from the lib2to3 copy of the reference in the
