@@ -80,7 +80,9 @@ def spawn_ranks(n, argv, script=None):
     never execs.  Rank 0 inherits stdout (it prints the JSON line); the other
     ranks' stdout goes to stderr.  When a rank fails, the others are
     terminated.  Returns the exit status: 0, or the first failing rank's."""
-    if os.environ.get('MAGOT_DIST_BACKEND') != 'gloo':
+    # an explicit MAGOT_DIST_BACKEND (gloo, or nccl where RCCL accepts ranks
+    # sharing a device) rehearses N ranks on fewer GPUs
+    if os.environ.get('MAGOT_DIST_BACKEND') not in ('gloo', 'nccl'):
         import torch
         ndev = torch.cuda.device_count()
         if n > ndev:
@@ -811,7 +813,7 @@ def main(argv=None):
     if world != args.gpus:
         log('--gpus %d but WORLD_SIZE=%d: running %d rank(s)' % (args.gpus, world, world))
     dist, rank, local, world = dist_setup()
-    if os.environ.get('MAGOT_DIST_BACKEND') == 'gloo':
+    if os.environ.get('MAGOT_DIST_BACKEND') in ('gloo', 'nccl'):
         import torch
         local = local % max(torch.cuda.device_count(), 1)
     os.environ.setdefault('MAGOT_DEVICE', str(local))
