@@ -80,9 +80,9 @@ def spawn_ranks(n, argv, script=None):
     never execs.  Rank 0 inherits stdout (it prints the JSON line); the other
     ranks' stdout goes to stderr.  When a rank fails, the others are
     terminated.  Returns the exit status: 0, or the first failing rank's."""
-    # an explicit MAGOT_DIST_BACKEND (gloo, or nccl where RCCL accepts ranks
-    # sharing a device) rehearses N ranks on fewer GPUs
-    if os.environ.get('MAGOT_DIST_BACKEND') not in ('gloo', 'nccl'):
+    # MAGOT_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (RCCL refuses
+    # ranks sharing a device: profiles/r04r/rccl_probe.json)
+    if os.environ.get('MAGOT_DIST_BACKEND') != 'gloo':
         import torch
         ndev = torch.cuda.device_count()
         if n > ndev:
@@ -159,8 +159,9 @@ def _reduce(dist, x, op):
     if dist is None:
         return x
     import torch
-    dev = 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
-    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+
+    from magot_amd.shard import collective_device
+    t = torch.tensor([float(x)], dtype=torch.float64, device=collective_device(dist))
     dist.all_reduce(t, op=op)
     return float(t.item())
 
@@ -734,7 +735,8 @@ def gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx):
         g_ln = shard.gather_offsets(dist, rank, world, ln)
         offs.append(list(zip(g_st, g_ln)) if rank == 0 else None)
     res = {'seconds': t_gather, 'bytes': int(allreduce_sum(dist, float(sum(it[1] for it in items)))),
-           'backend': dist.get_backend(), 'outputs': [it[0] for it in items]}
+           'backend': dist.get_backend(), 'collective_tensors': shard.collective_device(dist),
+           'outputs': [it[0] for it in items]}
     if rank != 0:
         return res
     t0 = time.perf_counter()
@@ -813,7 +815,7 @@ def main(argv=None):
     if world != args.gpus:
         log('--gpus %d but WORLD_SIZE=%d: running %d rank(s)' % (args.gpus, world, world))
     dist, rank, local, world = dist_setup()
-    if os.environ.get('MAGOT_DIST_BACKEND') in ('gloo', 'nccl'):
+    if os.environ.get('MAGOT_DIST_BACKEND') == 'gloo':
         import torch
         local = local % max(torch.cuda.device_count(), 1)
     os.environ.setdefault('MAGOT_DEVICE', str(local))

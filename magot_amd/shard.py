@@ -21,6 +21,8 @@ RCCL over xGMI on MI355X.  The job:
 With the gloo backend (CPU tests) the same steps run with host tensors.
 """
 
+import os
+
 import numpy as np
 
 
@@ -87,8 +89,16 @@ def imbalance(load):
     return float(load.max() / max(load.mean(), 1e-300) - 1.0) if len(load) else 0.0
 
 
-def _device(dist):
-    return 'cuda' if dist.get_backend() == 'nccl' else 'cpu'
+def collective_device(dist):
+    """Where collective operands live: the device with nccl (RCCL moves
+    device memory over xGMI), host memory with gloo.  MAGOT_COLLECTIVE_TENSORS=cuda
+    hands gloo device tensors instead (it stages them itself), so a one-GPU
+    rehearsal runs the same device-tensor code the nccl job runs; RCCL itself
+    refuses two ranks on one device."""
+    if dist.get_backend() == 'nccl' or os.environ.get('MAGOT_COLLECTIVE_TENSORS') == 'cuda':
+        return 'cuda'
+    return 'cpu'
+
 
 
 def replicate_genome(dist, rank, contigs, ctx):
@@ -114,7 +124,7 @@ def replicate_genome(dist, rank, contigs, ctx):
         info = [None, None, None, None, None]
     dist.broadcast_object_list(info, src=0)
     meta, nbytes, names, lengths, ranges = info
-    where = _device(dist)
+    where = collective_device(dist)
     buf = torch.empty(nbytes, dtype=torch.uint8, device='cuda')
     if rank == 0:
         dev.copy_arena(buf.data_ptr())
@@ -149,7 +159,7 @@ class Gather(object):
     def __init__(self, dist, rank, world, nbytes, device='cuda'):
         import torch
         self.dist, self.rank, self.world = dist, rank, world
-        where = _device(dist)
+        where = collective_device(dist)
         self.staged = where != 'cuda'
         sizes = torch.tensor([int(nbytes)], dtype=torch.int64, device=where)
         all_sizes = [torch.zeros(1, dtype=torch.int64, device=where) for _ in range(world)]
@@ -205,7 +215,7 @@ def gather_offsets(dist, rank, world, off):
     arrays on rank 0, None elsewhere."""
     import torch
     off = np.ascontiguousarray(off, dtype=np.int64)
-    where = _device(dist)
+    where = collective_device(dist)
     n = torch.tensor([len(off)], dtype=torch.int64, device=where)
     ns = [torch.zeros(1, dtype=torch.int64, device=where) for _ in range(world)]
     dist.all_gather(ns, n)

@@ -40,7 +40,7 @@ if has c5; then
 fi
 if has multi5; then
   # the C5 job over two ranks sharing the card (gloo): six-frame outputs gathered back
-  MAGOT_DIST_BACKEND=gloo timeout -k 10 900 python $BENCH --gpus 2 --config C5 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo2_c5.json 2> $OUT/gloo2_c5.err || { tail -30 $OUT/gloo2_c5.err; exit 1; }
+  MAGOT_DIST_BACKEND=gloo MAGOT_COLLECTIVE_TENSORS=cuda timeout -k 10 900 python $BENCH --gpus 2 --config C5 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo2_c5.json 2> $OUT/gloo2_c5.err || { tail -30 $OUT/gloo2_c5.err; exit 1; }
   grep '^{' $OUT/bench_gloo2_c5.json | cut -c1-400
 fi
 if has e2e; then
@@ -51,7 +51,7 @@ fi
 if has multi; then
   # two ranks launched by bench itself, sharing the one card over gloo (the
   # C4 orchestration; the driver's 8-GPU node runs it over RCCL)
-  MAGOT_DIST_BACKEND=gloo timeout -k 10 600 python $BENCH --gpus 2 --steps 50 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo2.json 2> $OUT/gloo2.err || { tail -30 $OUT/gloo2.err; exit 1; }
+  MAGOT_DIST_BACKEND=gloo MAGOT_COLLECTIVE_TENSORS=cuda timeout -k 10 600 python $BENCH --gpus 2 --steps 50 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo2.json 2> $OUT/gloo2.err || { tail -30 $OUT/gloo2.err; exit 1; }
   grep '^{' $OUT/bench_gloo2.json
 fi
 if has kt; then

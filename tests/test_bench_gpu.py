@@ -1,7 +1,9 @@
 """bench.py end to end on the GPU at test size: the one-rank job and the
 multi-rank C4 path that ``python bench.py --gpus N`` launches itself (two
 ranks rehearsed on one card with MAGOT_DIST_BACKEND=gloo; the RCCL path is the
-same code with the nccl backend, one GPU per rank).  Each rank checks its own
+same code with the nccl backend, one GPU per rank; RCCL refuses two ranks on
+one device, so MAGOT_COLLECTIVE_TENSORS=cuda rehearses its device-tensor
+collectives through gloo).  Each rank checks its own
 shard against the C oracle, and rank 0 checks the outputs gathered from every
 rank in global record order."""
 
@@ -45,9 +47,13 @@ def test_bench_one_rank():
     assert probe['store_gbs'] > 100 and probe['copy_gbs'] > 100
 
 
-def test_bench_spawns_two_ranks_strong():
+@pytest.mark.parametrize('tensors', ['cpu', 'cuda'])
+def test_bench_spawns_two_ranks_strong(tensors):
+    """The C4 job over two ranks; 'cuda': the genome broadcast, the size
+    exchanges and the output gather take device tensors, as under nccl."""
     d = _bench(['--gpus', '2', '--config', 'small'] + COMMON,
-               {'MAGOT_DIST_BACKEND': 'gloo'})
+               {'MAGOT_DIST_BACKEND': 'gloo', 'MAGOT_COLLECTIVE_TENSORS': tensors})
+    assert d['outputs_gather']['collective_tensors'] == tensors
     assert d['n_gpus'] == 2 and d['scaling'] == 'strong'
     assert d['parity'].startswith('bit-exact'), d['parity']
     assert d['outputs_gather']['parity'].startswith('bit-exact'), d['outputs_gather']
@@ -64,11 +70,12 @@ def test_bench_spawns_two_ranks_weak():
 
 
 def test_bench_spawns_eight_ranks_strong():
-    """The world-8 job end to end (eight gloo ranks sharing this card): the
-    8-way sharding, the wire broadcast of the genome, every rank's shard
+    """The world-8 job end to end (eight gloo ranks sharing this card, device
+    tensors handed to the collectives as under nccl): the 8-way sharding, the wire broadcast of the genome, every rank's shard
     checked, the 8-part gather and the reassembly in global record order."""
-    d = _bench(['--gpus', '8', '--config', 'small'] + COMMON, {'MAGOT_DIST_BACKEND': 'gloo'})
-    assert d['n_gpus'] == 8
+    d = _bench(['--gpus', '8', '--config', 'small'] + COMMON,
+               {'MAGOT_DIST_BACKEND': 'gloo', 'MAGOT_COLLECTIVE_TENSORS': 'cuda'})
+    assert d['n_gpus'] == 8 and d['outputs_gather']['collective_tensors'] == 'cuda'
     assert d['parity'].startswith('bit-exact'), d['parity']
     g = d['outputs_gather']
     assert g['parity'].startswith('bit-exact') and 'global record order' in g['parity'], g
@@ -76,10 +83,14 @@ def test_bench_spawns_eight_ranks_strong():
     assert d['host']['peak_rss_gib_max_rank'] > 0
 
 
-def test_bench_six_frame_job_two_ranks():
+@pytest.mark.parametrize('tensors', ['cpu', 'cuda'])
+def test_bench_six_frame_job_two_ranks(tensors):
     """The C5 job over two ranks: six-frame streams gathered and put back into
-    the single-GPU layout, all six frames of every record checked."""
-    d = _bench(['--gpus', '2', '--config', 'small5'] + COMMON, {'MAGOT_DIST_BACKEND': 'gloo'})
+    the single-GPU layout, all six frames of every record checked; with
+    device tensors handed to the collectives, as under nccl."""
+    d = _bench(['--gpus', '2', '--config', 'small5'] + COMMON,
+               {'MAGOT_DIST_BACKEND': 'gloo', 'MAGOT_COLLECTIVE_TENSORS': tensors})
+    assert d['outputs_gather']['collective_tensors'] == tensors
     assert d['roofline']['kernel'] == 'orf6_kernel'
     assert d['parity'].startswith('bit-exact'), d['parity']
     g = d['outputs_gather']
