@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 ENVS=()
 while [ $# -gt 0 ] && [ "$1" != "--" ]; do ENVS+=("$1"); shift; done
 [ "$1" = "--" ] && shift
-OUT=gpurun_out/abenvs; mkdir -p $OUT
+OUT=${AB_OUT:-gpurun_out/abenvs}; mkdir -p $OUT
 for i in 1 2 3; do
   k=0
   for e in "${ENVS[@]}"; do
