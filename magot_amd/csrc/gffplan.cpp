@@ -431,13 +431,17 @@ void detect_format(GffFormat& F, sv tags_text) {
 // The de-duplicated name of the r-th line (r >= 2) holding an existing ID
 // (genome.py:330-338): ID2, then ID-3, ID-4 ...
 inline void dup_name(sv id, uint32_t j, std::string& out) {
-  out.assign(id.data(), id.size());
+  char buf[16];
+  char* e = buf + sizeof buf;
+  char* p = e;
   if (j == 1) {
-    out += '2';
+    *--p = '2';
   } else {
-    out += '-';
-    out += std::to_string(j + 1);
+    for (uint32_t v = j + 1; v; v /= 10) *--p = (char)('0' + v % 10);
+    *--p = '-';
   }
+  out.assign(id.data(), id.size());
+  out.append(p, (size_t)(e - p));
 }
 
 struct LineParser {
