@@ -403,6 +403,22 @@ typedef struct magot_gffplan magot_gffplan;
 int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
                    const uint64_t* contig_lens, uint32_t n_contigs, const char* feature,
                    uint32_t flags, magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx);
+/*
+ * extract_upstream_downstream (genome_tools.py:457-480) as a plan of the same
+ * shape: one single-interval record per printed window (the `sequence_length`
+ * bases before a '+' feature for stream "up", after it reverse-complemented
+ * for "down"; mirrored on '-'), names from the last `namefrom=` attribute or
+ * "seq<k>", a matching line whose strand is neither '+' nor '-' repeating the
+ * previous window, windows shorter than sequence_length dropped, records
+ * joined by "\n".  Render it with magot_gffplan_render or magot_fasta_text_*
+ * like a gff2fasta plan (nucleotide).  sequence_length is the reference's
+ * string argument.  MAGOT_ERR_UNSUPPORTED when the reference would raise
+ * (unknown seqid, a bad integer, `namefrom` without '=', no window yet).
+ */
+int magot_flank_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
+                     const uint64_t* contig_lens, uint32_t n_contigs, const char* feature_type,
+                     const char* namefrom, const char* sequence_length, const char* stream,
+                     magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx);
 /* Copy the planned tables (n_exons / n_tx entries from magot_gff_plan). */
 int magot_gffplan_tables(const magot_gffplan* p, magot_exon* exons, magot_tx* txs);
 /* The FASTA text: skeleton + record payloads from magot_plan_fetch (nuc for

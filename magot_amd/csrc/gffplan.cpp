@@ -1194,6 +1194,194 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
   return MAGOT_OK;
 }
 
+// extract_upstream_downstream (genome_tools.py:457-480) lowered to the same
+// plan shape as gff2fasta: one single-interval record per printed window and
+// a skeleton ">" name "\n" [record] joined by "\n".  Lines are scanned in
+// parallel chunks; the output count ('seq' + count names) and the quirk that a
+// matching line with a strand other than '+' / '-' prints the previous
+// window again are resolved in one ordered pass.  Every reference error path
+// (KeyError, ValueError, IndexError, UnboundLocalError) declines.
+int magot_flank_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
+                     const uint64_t* contig_lens, uint32_t n_contigs, const char* feature_type,
+                     const char* namefrom, const char* sequence_length, const char* stream,
+                     magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx) {
+  using magot::sv;
+  if (!out || (gff_len && !gff) || (n_contigs && (!seqids || !contig_lens)) || !feature_type ||
+      !namefrom || !sequence_length || !stream) {
+    magot::set_error("magot_flank_plan: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  std::unique_ptr<magot_gffplan> P(new magot_gffplan());
+  // one matching line: a window of its own, or the previous one again
+  struct Hit {
+    uint64_t start;
+    uint32_t contig, len;
+    bool own, rc, has_name;
+    sv name;  // into the GFF text; "\r" / "\n" still inside
+  };
+  try {
+    const int64_t n = magot::parse_int(sv(sequence_length));  // int(sequence_length)
+    const sv ftype(feature_type), key(namefrom), st(stream);
+    const bool up = st == "up", down = st == "down";
+    std::unordered_map<sv, uint32_t> contig_of;
+    for (uint32_t i = 0; i < n_contigs; ++i) contig_of[sv(seqids[i])] = i;  // last duplicate wins
+    unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    uint64_t n_chunks = gff_len < (1u << 20) ? 1 : std::min<uint64_t>(hw * 8ull, gff_len >> 16);
+    if (const char* e = std::getenv("MAGOT_GFF_CHUNKS"))  // test hook: force the split
+      n_chunks = std::max<uint64_t>(1, std::min<uint64_t>(strtoull(e, nullptr, 10), gff_len));
+    std::vector<uint64_t> cut(n_chunks + 1, gff_len);
+    cut[0] = 0;
+    for (uint64_t c = 1; c < n_chunks; ++c) {
+      const uint64_t p = std::max(cut[c - 1], gff_len * c / n_chunks);
+      const char* nl =
+          p ? static_cast<const char*>(memchr(gff + p - 1, '\n', gff_len - p + 1)) : gff;
+      cut[c] = !nl ? gff_len : (p ? (uint64_t)(nl - gff) + 1 : 0);
+    }
+    std::vector<std::vector<Hit>> hits(n_chunks);
+    magot::FirstError failed;
+    std::atomic<bool> unsupported{false};
+    std::atomic<uint64_t> next{0};
+    auto work = [&]() {
+      for (uint64_t c; (c = next.fetch_add(1)) < n_chunks && !unsupported.load();) {
+        try {
+          for (uint64_t pos = cut[c]; pos < cut[c + 1];) {
+            // `for line in open(gff)`: lines end after '\n', which they keep
+            const char* nl = static_cast<const char*>(memchr(gff + pos, '\n', cut[c + 1] - pos));
+            const uint64_t end = nl ? (uint64_t)(nl - gff) + 1 : cut[c + 1];
+            const sv line(gff + pos, end - pos);
+            pos = end;
+            if (line.empty() || line[0] == '#') continue;
+            // fields = line.split('\t'), needed when line.count('\t') > 5
+            uint32_t tab[8];
+            int tabs = 0;
+            size_t last = 0;
+            for (size_t i = 0; i < line.size(); ++i)
+              if (line[i] == '\t') {
+                if (tabs < 8) tab[tabs] = (uint32_t)i;
+                ++tabs;
+                last = i;
+              }
+            if (tabs < 6) continue;
+            auto field = [&](int k) {  // k <= 6; fields[6] may be the last one
+              const size_t b = k ? tab[k - 1] + 1 : 0;
+              const size_t e = k < tabs ? tab[k] : line.size();
+              return line.substr(b, e - b);
+            };
+            if (field(2) != ftype) continue;
+            int64_t lo = magot::parse_int(field(3)), hi = magot::parse_int(field(4));
+            if (lo > hi) std::swap(lo, hi);
+            Hit h{};
+            // the last attribute whose text before its first '=' is namefrom;
+            // its name is the text between the first and second '='
+            const sv attrs = line.substr(last + 1);
+            for (size_t b = 0;;) {
+              const size_t e = attrs.find(';', b);
+              const sv a = attrs.substr(b, e == sv::npos ? sv::npos : e - b);
+              const size_t q = a.find('=');
+              if (a.substr(0, q) == key) {
+                if (q == sv::npos) throw Unsupported();  // IndexError
+                const size_t q2 = a.find('=', q + 1);
+                h.name = a.substr(q + 1, q2 == sv::npos ? sv::npos : q2 - q - 1);
+                h.has_name = true;
+              }
+              if (e == sv::npos) break;
+              b = e + 1;
+            }
+            const sv strand = field(6);
+            const bool plus = strand == "+", minus = strand == "-";
+            int64_t a = 0, b = 0;
+            if ((up && plus) || (down && minus)) {  // stop - n .. stop, as printed
+              a = lo - 1 - n;
+              b = lo - 1;
+              h.own = true;
+            } else if ((down && plus) || (up && minus)) {  // start .. start + n, reverse complement
+              a = hi;
+              b = hi + n;
+              h.own = h.rc = true;
+            }
+            if (h.own) {
+              const auto ci = contig_of.find(field(0));
+              if (ci == contig_of.end()) throw Unsupported();  // KeyError
+              const int64_t L = (int64_t)contig_lens[ci->second];
+              auto norm = [&](int64_t x) { return x < 0 ? std::max<int64_t>(x + L, 0) : std::min(x, L); };
+              const int64_t s = norm(a), e = norm(b);
+              const uint64_t ln = (uint64_t)std::max<int64_t>(0, e - s);
+              if (ln >= 0xFFFFFFFFull) throw Unsupported();
+              h.start = (uint64_t)s;
+              h.len = (uint32_t)ln;
+              h.contig = ci->second;
+            }
+            hits[c].push_back(h);
+          }
+        } catch (const Unsupported&) {
+          unsupported = true;
+        } catch (...) {
+          failed.set();
+          unsupported = true;
+        }
+      }
+    };
+    {
+      std::vector<std::thread> pool;
+      for (unsigned t = 1; t < std::min<uint64_t>(hw, n_chunks); ++t) pool.emplace_back(work);
+      work();
+      for (auto& t : pool) t.join();
+    }
+    failed.rethrow();
+    if (unsupported) throw Unsupported();
+    // ordered pass: names, the reused window, "\n".join(output_seqs)
+    bool bound = false;
+    Hit cur{};
+    uint64_t count = 0;
+    char num[24];
+    for (const auto& V : hits)
+      for (const Hit& h : V) {
+        if (h.own) {
+          cur = h;
+          bound = true;
+        } else if (!bound) {
+          throw Unsupported();  // UnboundLocalError
+        }
+        if (n < 0 || (int64_t)cur.len != n) continue;
+        const uint64_t t0 = P->text.size();
+        if (count) P->text += '\n';
+        P->text += '>';
+        if (h.has_name) {
+          for (char ch : h.name)
+            if (ch != '\r' && ch != '\n') P->text += ch;
+        } else {
+          const int k = snprintf(num, sizeof num, "seq%llu", (unsigned long long)count);
+          P->text.append(num, (size_t)k);
+        }
+        P->text += '\n';
+        P->pieces.push_back({t0, P->text.size() - t0, -1});
+        magot_tx t;
+        t.exon_begin = P->exons.size();
+        t.n_exons = 1;
+        t.flags = 0;
+        magot_exon x;
+        x.start_rc = cur.start | (cur.rc ? magot::kRcBit : 0);
+        x.contig = cur.contig;
+        x.len = cur.len;
+        P->exons.push_back(x);
+        P->pieces.push_back({0, 0, (int64_t)P->txs.size()});
+        P->txs.push_back(t);
+        ++count;
+      }
+  } catch (const Unsupported&) {
+    magot::set_error("magot_flank_plan: input takes a diagnostic path; use the object path");
+    return MAGOT_ERR_UNSUPPORTED;
+  } catch (const std::exception& e) {
+    magot::set_error(std::string("magot_flank_plan: ") + e.what());
+    return MAGOT_ERR_ARG;
+  }
+  if (n_exons) *n_exons = P->exons.size();
+  if (n_tx) *n_tx = P->txs.size();
+  *out = P.release();
+  return MAGOT_OK;
+}
+
 int magot_gffplan_tables(const magot_gffplan* p, magot_exon* exons, magot_tx* txs) {
   if (!p) {
     magot::set_error("magot_gffplan_tables: null plan");

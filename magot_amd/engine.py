@@ -490,6 +490,30 @@ class GffPlan(object):
         check(rc, 'magot_gff_plan')
         return cls(h, ne.value, nt.value, protein and not genomic)
 
+    @classmethod
+    def flank(cls, gff, names, lengths, sequence_length, stream, feature_type='gene',
+              namefrom='ID'):
+        """extract_upstream_downstream's windows (genome_tools.py:457-480,
+        magot_flank_plan) as a nucleotide plan: one single-interval record per
+        printed window, the same skeleton shape as gff2fasta.  None when the
+        reference would raise (the caller's line loop reproduces it).
+        ``sequence_length`` and ``stream`` are the reference's strings."""
+        L = _lib.lib()
+        text = _text_view(gff)
+        n = len(names)
+        arr = (ctypes.c_char_p * max(n, 1))(*[_as_bytes(x) for x in names])
+        lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+        h = ctypes.c_void_p()
+        ne, nt = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = L.magot_flank_plan(_text_ptr(text), len(text), arr, lens.ctypes.data_as(_lib._u64p),
+                                n, _as_bytes(feature_type), _as_bytes(namefrom),
+                                _as_bytes(str(sequence_length)), _as_bytes(stream),
+                                ctypes.byref(h), ctypes.byref(ne), ctypes.byref(nt))
+        if rc == _lib.ERR_UNSUPPORTED:
+            return None
+        check(rc, 'magot_flank_plan')
+        return cls(h, ne.value, nt.value, False)
+
     def render(self, nuc, noff, pep, poff):
         """The FASTA text (bytes) around the fetched record payloads."""
         L = _lib.lib()

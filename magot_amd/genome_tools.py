@@ -5,7 +5,7 @@
            [native=False]
     python -m magot_amd.genome_tools cds2pep <cds.fasta>
     python -m magot_amd.genome_tools extract_upstream_downstream <fasta> <gff> <length> up|down
-           [feature_type=gene] [namefrom=ID] [truncate_names=True]
+           [feature_type=gene] [namefrom=ID] [truncate_names=True] [native=False]
     python -m magot_amd.genome_tools coords2fasta <fasta> <seqid> <start> <stop> [truncate_names=False]
     python -m magot_amd.genome_tools blast_csv2fasta <fasta> <blast.csv> [order=py2|insertion]
     python -m magot_amd.genome_tools exonerate2fasta <fasta> <exonerate.txt> [order=py2|insertion]
@@ -256,14 +256,26 @@ def _gather(seqs, intervals):
 
 
 def extract_upstream_downstream(genome_sequence, gff, sequence_length, stream,
-                                feature_type='gene', namefrom='ID', truncate_names='True'):
+                                feature_type='gene', namefrom='ID', truncate_names='True',
+                                native='True'):
     """genome_tools.py:457-480: the `sequence_length` bases up- or downstream of
-    every `feature_type` line, strand-aware, gathered on the GPU in one batch.
-    Reference quirks kept: 'down' on '+' and 'up' on '-' are reverse
-    complemented; a strand other than '+'/'-' reuses the previous line's
-    sequence (or raises UnboundLocalError); only full-length windows print."""
-    seqs = genome.GenomeSequence(genome_sequence, truncate_names=_literal(truncate_names))
-    n = int(sequence_length)
+    every `feature_type` line, strand-aware.  Reference quirks kept: 'down' on
+    '+' and 'up' on '-' are reverse complemented; a strand other than '+'/'-'
+    reuses the previous line's sequence (or raises UnboundLocalError); only
+    full-length windows print.
+
+    Natively (magot_flank_plan: the GFF scanned in C++, the windows gathered
+    by the extraction kernel, the FASTA text assembled on the device) unless
+    the input would take one of the reference's error paths, which the line
+    loop below reproduces (``native=False`` forces it)."""
+    truncate = _literal(truncate_names)
+    if native == 'True' and isinstance(truncate, bool):
+        text = _flank_native(genome_sequence, gff, sequence_length, stream, feature_type,
+                             namefrom, truncate)
+        if text is not None:
+            _write_bytes(text, b'\n')
+            return
+    seqs = genome.GenomeSequence(genome_sequence, truncate_names=truncate)
     index = {name: i for i, name in enumerate(seqs)}
     current = None
     items = []
@@ -283,19 +295,50 @@ def extract_upstream_downstream(genome_sequence, gff, sequence_length, stream,
                     name = 'seq' + str(len(items))
                 if stream == 'up' and fields[6] == '+' or stream == 'down' and fields[6] == '-':
                     stop = coords[0] - 1
+                    n = int(sequence_length)
                     st, ln = genome._slice_interval(seqs[fields[0]], stop - n, stop)
                     current = (index[fields[0]], st, ln, False)
                 elif stream == 'down' and fields[6] == '+' or stream == 'up' and fields[6] == '-':
                     start = coords[1]
+                    n = int(sequence_length)
                     st, ln = genome._slice_interval(seqs[fields[0]], start, start + n)
                     current = (index[fields[0]], st, ln, True)
                 if current is None:
                     raise UnboundLocalError(
                         "local variable 'sequence' referenced before assignment")
-                if current[2] == n:
+                if current[2] == int(sequence_length):
                     items.append((name, current))
     texts = _gather(seqs, [iv for _, iv in items])
     _write('\n'.join('>' + name + '\n' + t for (name, _), t in zip(items, texts)) + '\n')
+
+
+def _flank_native(genome_sequence, gff, sequence_length, stream, feature_type, namefrom,
+                  truncate):
+    """extract_upstream_downstream's text (bytes, no final newline) via
+    magot_flank_plan, one extraction launch and device text assembly; None
+    when the FASTA needs the Python reader or the input takes an error path."""
+    dev = engine.FastaGenome.load(genome.read_buffer(genome_sequence), truncate_names=truncate)
+    if dev is None:
+        return None
+    plan = engine.GffPlan.flank(genome.read_buffer(gff), dev.names,
+                                [int(x) for x in dev.lengths], sequence_length, stream,
+                                feature_type=feature_type, namefrom=namefrom)
+    if plan is None:
+        return None
+    try:
+        if len(plan.txs) == 0:
+            return b''
+        ex = engine.ExtractionPlan(dev, plan.exons, plan.txs, engine.OUT_NUC)
+        text = engine.FastaText(plan, ex)
+        try:
+            ex.execute()
+            text.execute()
+            return text.fetch()
+        finally:
+            text.close()
+            ex.close()
+    finally:
+        plan.close()
 
 
 def coords2fasta(fasta_file, seqid, start, stop, truncate_names='False'):
