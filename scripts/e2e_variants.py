@@ -1,5 +1,6 @@
 """Times gff2fasta's longest=True (nucleotide and protein) and genomic=True variants,
-and cds2pep over the nucleotide output, on the native path
+cds2pep over the nucleotide output, and extract_upstream_downstream (1 kb up /
+down of every gene), on the native path against the line loops,
 over the files of an e2e_cli.py run (C3 by default), each in this process
 after one warm call of the default variant (device start-up excluded).
 Correctness of these variants is pinned by tests/test_gffplan.py (oracle) and
@@ -53,6 +54,22 @@ def main():
             's': time.perf_counter() - t, 'bytes': len(b.getvalue())}
         outs[native] = b.getvalue()
     rec['cds2pep_outputs_equal'] = outs['True'] == outs['False']
+    # extract_upstream_downstream (genome_tools.py:457-480): 1 kb windows
+    # before / after every gene, native (C++ scan + one extraction launch +
+    # device text) against the line loop (Python scan + the same launch)
+    for stream in ('up', 'down'):
+        outs = {}
+        for native in ('True', 'False'):
+            b = io.BytesIO()
+            w = io.TextIOWrapper(b, encoding='latin-1', write_through=True)
+            t = time.perf_counter()
+            with redirect_stdout(w):
+                genome_tools.extract_upstream_downstream(fa, gf, '1000', stream, native=native)
+            w.flush()
+            rec['flank_%s_%s' % (stream, 'native' if native == 'True' else 'line_loop')] = {
+                's': time.perf_counter() - t, 'bytes': len(b.getvalue())}
+            outs[native] = b.getvalue()
+        rec['flank_%s_outputs_equal' % stream] = outs['True'] == outs['False']
     print(json.dumps(rec), flush=True)
 
 
