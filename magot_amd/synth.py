@@ -104,9 +104,16 @@ class Workload(object):
                 out.append(s[p:p + width] + '\n')
         return ''.join(out)
 
-    def gff3_text(self):
+    def gff3_text(self, ids='synth'):
         """NCBI-like gene -> mRNA -> CDS; the CDS ID repeats within a transcript
-        so read_gff's renaming path runs (genome.py:355-364)."""
+        so read_gff's renaming path runs (genome.py:355-364).  ids='synth':
+        gene<t> / rna<t> / cds<t>, whose renamed CDS IDs (cds<t>2, cds<t>-3 ..)
+        collide with other transcripts' (cds52 is transcript 52's CDS and
+        transcript 5's second), so read_gff's renaming cascades; ids='ncbi':
+        gene-G<t> / rna-XM_<t>.1 / cds-XP_<t>.1 as NCBI's files name them,
+        whose renamed IDs never meet another ID."""
+        if ids == 'ncbi':
+            return self._gff3_ncbi()
         lines = ['##gff-version 3\n']
         first = np.concatenate([[0], np.cumsum(self.ex_count)])
         for t in range(self.n_tx):
@@ -126,6 +133,28 @@ class Workload(object):
                              % (c, s0, s1, st, t, e - a, t))
                 lines.append('%s\tsynth\tCDS\t%d\t%d\t.\t%s\t0\tID=cds%d;Parent=rna%d\n'
                              % (c, s0, s1, st, t, t))
+        return ''.join(lines)
+
+    def _gff3_ncbi(self):
+        lines = ['##gff-version 3\n']
+        first = np.concatenate([[0], np.cumsum(self.ex_count)])
+        for t in range(self.n_tx):
+            c = self.contig_names[self.tx_contig[t]]
+            st = '+' if self.tx_strand[t] > 0 else '-'
+            a, b = first[t], first[t + 1]
+            lo = int(self.ex_start[a]) + 1
+            hi = int(self.ex_start[b - 1] + self.ex_len[b - 1])
+            lines.append('%s\tsynth\tgene\t%d\t%d\t.\t%s\t.\tID=gene-G%07d;Name=G%d\n'
+                         % (c, lo, hi, st, t, t))
+            lines.append('%s\tsynth\tmRNA\t%d\t%d\t.\t%s\t.\tID=rna-XM_%09d.1;Parent=gene-G%07d\n'
+                         % (c, lo, hi, st, t, t))
+            for e in range(a, b):
+                s0 = int(self.ex_start[e]) + 1
+                s1 = int(self.ex_start[e] + self.ex_len[e])
+                lines.append('%s\tsynth\texon\t%d\t%d\t.\t%s\t.\tID=exon-XM_%09d.1-%d;'
+                             'Parent=rna-XM_%09d.1\n' % (c, s0, s1, st, t, e - a + 1, t))
+                lines.append('%s\tsynth\tCDS\t%d\t%d\t.\t%s\t0\tID=cds-XP_%09d.1;'
+                             'Parent=rna-XM_%09d.1\n' % (c, s0, s1, st, t, t))
         return ''.join(lines)
 
     def gtf_text(self):

@@ -26,6 +26,9 @@ def main():
     ap.add_argument('--seq-type', default='protein')
     ap.add_argument('--dir', default='/tmp/magot_e2e')
     ap.add_argument('--order', default='py2')
+    ap.add_argument('--ids', default='synth', choices=['synth', 'ncbi'],
+                    help="the GFF3's IDs: 'synth' (renamed CDS IDs collide, read_gff's "
+                         "renaming cascades) or 'ncbi' (NCBI-style, all distinct)")
     ap.add_argument('--whole', action='store_true',
                     help='time the CLI call (genome_tools._gff2fasta_native) on the files of '
                          'an earlier run, in this fresh process, and compare with its out.fa')
@@ -47,7 +50,7 @@ def main():
     with open(fa, 'w') as fh:
         fh.write(w.fasta_text())
     with open(gf, 'w') as fh:
-        fh.write(w.gff3_text())
+        fh.write(w.gff3_text(ids=a.ids))
     t_gen = time.perf_counter() - t
     ph = {}
     t0 = time.perf_counter()
@@ -118,7 +121,7 @@ def main():
         keep = np.ones(len(pep), dtype=bool)
         keep[starts[first]] = False
         ok = bool(np.array_equal(pep[keep], ref))
-    rec = {'config': a.config, 'seq_type': a.seq_type, 'order': a.order,
+    rec = {'config': a.config, 'seq_type': a.seq_type, 'order': a.order, 'ids': a.ids,
            'records': int(len(plan.txs)), 'intervals': int(len(plan.exons)),
            'cds_bases': int(w.cds_bases), 'output_bytes': len(text) + 1,
            'gff_lines': None, 'phases_s': ph, 'end_to_end_s': total,
