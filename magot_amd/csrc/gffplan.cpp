@@ -220,6 +220,10 @@ struct Model {
         if (best < 0 || rank[t] > rank[(uint32_t)best]) best = (int)t;
     return slot((uint32_t)best, idk);
   }
+  int64_t lookup(sv s) const {
+    const int64_t k = ids.find(s);
+    return k < 0 ? -1 : lookup((uint32_t)k);
+  }
   // table[ID] = feature (a dict assignment: an existing key keeps its position)
   void put(uint32_t t, uint32_t idk, uint32_t f) {
     const uint64_t m = id_types[idk];
@@ -547,221 +551,6 @@ struct LineParser {
   }
 };
 
-// string -> uint32 for the parallel ordered pass: open addressing over
-// precomputed hashes, sized once (load <= 1/2), no per-entry allocation.
-struct FlatMap {
-  struct Slot {
-    uint64_t h;
-    sv key;
-    uint32_t val;
-    bool used;
-  };
-  std::vector<Slot> slots;
-  size_t mask = 0;
-  explicit FlatMap(size_t n) {
-    size_t cap = 16;
-    while (cap < 2 * n + 2) cap <<= 1;
-    slots.assign(cap, Slot{0, sv(), 0, false});
-    mask = cap - 1;
-  }
-  // the entry of `key` (inserted with `val` when absent); `fresh` says which
-  Slot& get(sv key, uint64_t h, uint32_t val, bool* fresh) {
-    for (size_t i = (size_t)(h ^ (h >> 29)) & mask;; i = (i + 1) & mask) {
-      Slot& s = slots[i];
-      if (!s.used) {
-        s = Slot{h, key, val, true};
-        *fresh = true;
-        return s;
-      }
-      if (s.h == h && s.key == key) {
-        *fresh = false;
-        return s;
-      }
-    }
-  }
-  const Slot* find(sv key, uint64_t h) const {
-    for (size_t i = (size_t)(h ^ (h >> 29)) & mask;; i = (i + 1) & mask) {
-      const Slot& s = slots[i];
-      if (!s.used) return nullptr;
-      if (s.h == h && s.key == key) return &s;
-    }
-  }
-};
-
-// Runs fn(0 .. n-1) over up to hw threads; false if any call threw.
-template <class Fn>
-bool par_for(unsigned hw, size_t n, Fn fn) {
-  std::atomic<size_t> next{0};
-  std::atomic<bool> bad{false};
-  auto work = [&]() {
-    for (size_t t; (t = next.fetch_add(1)) < n && !bad.load();) {
-      try {
-        fn(t);
-      } catch (...) {
-        bad = true;
-      }
-    }
-  };
-  std::vector<std::thread> pool;
-  for (unsigned t = 1; t < std::min<size_t>(hw, n); ++t) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
-  return !bad.load();
-}
-
-// The ordered pass of read_gff, in parallel, for GFF3 without a hierarchy
-// whose final IDs are all distinct (the common shape: every ID once, or
-// repeated only where the renaming below keeps names apart).  Then the
-// file-order semantics reduce to:
-//  - the j-th repeat (j >= 1) of an ID is renamed ID2 / ID-(j+1)
-//    (genome.py:330-338), and line i's ID is the i-th interned string;
-//  - line i's feature is feats[i], stored under ID i in its type's table;
-//  - a parent is the line whose final ID equals the Parent value and that
-//    precedes the child; the child joins its child list in file order.
-// Anything else (a collision between final IDs, a parent defined later or
-// not at all, a base-type parent, a hierarchy) returns false with the model
-// untouched, and the sequential pass decides, including its diagnostics.
-bool ordered_pass_distinct(Model& M, const GffFormat& F,
-                           const std::vector<std::vector<GffLine>>& lines,
-                           const std::vector<std::unique_ptr<LineParser>>& parsers, unsigned hw) {
-  if (!F.hierarchy.empty() || std::getenv("MAGOT_GFF_ORDERED")) return false;
-  const size_t n_chunks = lines.size();
-  std::vector<uint64_t> base(n_chunks + 1, 0);
-  for (size_t c = 0; c < n_chunks; ++c) base[c + 1] = base[c] + lines[c].size();
-  const uint64_t NL = base[n_chunks];
-  if (NL == 0 || NL >= 0xFFFFFFFFull) return false;
-  constexpr unsigned kParts = 64;
-  auto part = [](uint64_t h) { return (unsigned)(h >> 58); };
-  // lines by the partition of their original ID / of their Parent value
-  std::vector<std::vector<std::vector<uint32_t>>> by_id(n_chunks), by_par(n_chunks);
-  if (!par_for(hw, n_chunks, [&](size_t c) {
-        by_id[c].resize(kParts);
-        by_par[c].resize(kParts);
-        for (size_t k = 0; k < lines[c].size(); ++k) {
-          const GffLine& L = lines[c][k];
-          const uint32_t i = (uint32_t)(base[c] + k);
-          by_id[c][part(L.h_id)].push_back(i);
-          if (L.has_parent) by_par[c][part(L.h_parent)].push_back(i);
-        }
-      }))
-    return false;
-  // final IDs: occurrence counts per original ID, in file order
-  std::vector<sv> name(NL);
-  std::vector<uint64_t> hname(NL);
-  std::vector<Arena> renames(kParts);
-  std::vector<std::vector<std::vector<uint32_t>>> by_name(kParts);
-  if (!par_for(hw, kParts, [&](size_t p) {
-        size_t cnt = 0;
-        for (size_t c = 0; c < n_chunks; ++c) cnt += by_id[c][p].size();
-        FlatMap seen(cnt);
-        std::string tmp;
-        by_name[p].resize(kParts);
-        for (size_t c = 0; c < n_chunks; ++c)
-          for (uint32_t i : by_id[c][p]) {
-            const GffLine& L = lines[c][i - base[c]];
-            bool fresh;
-            const uint32_t j = seen.get(L.id, L.h_id, 0, &fresh).val++;
-            if (j == 0) {
-              name[i] = L.id;
-              hname[i] = L.h_id;
-            } else {
-              dup_name(L.id, j, tmp);
-              name[i] = renames[p].join({sv(tmp)});
-              hname[i] = hash_sv(name[i]);
-            }
-            by_name[p][part(hname[i])].push_back(i);
-          }
-      }))
-    return false;
-  // distinct final IDs, and every Parent resolved to an earlier line
-  std::vector<int64_t> parent(NL, -1);
-  std::atomic<bool> clash{false};
-  if (!par_for(hw, kParts, [&](size_t q) {
-        size_t cnt = 0;
-        for (size_t p = 0; p < kParts; ++p) cnt += by_name[p][q].size();
-        FlatMap where(cnt);
-        for (size_t p = 0; p < kParts && !clash.load(); ++p)
-          for (uint32_t i : by_name[p][q]) {
-            bool fresh;
-            where.get(name[i], hname[i], i, &fresh);
-            if (!fresh) {
-              clash = true;
-              return;
-            }
-          }
-        for (size_t c = 0; c < n_chunks && !clash.load(); ++c)
-          for (uint32_t i : by_par[c][q]) {
-            const GffLine& L = lines[c][i - base[c]];
-            const FlatMap::Slot* it = where.find(L.parent, L.h_parent);
-            if (!it || it->val >= i) {
-              clash = true;
-              return;
-            }
-            parent[i] = it->val;
-          }
-      }) ||
-      clash.load())
-    return false;
-  // seqids, strands and tables, each in its own first-seen order (a chunk's
-  // local codes are in first-seen order within the chunk)
-  std::vector<std::vector<uint32_t>> sq_of(n_chunks), st_of(n_chunks), ty_of(n_chunks);
-  std::vector<std::vector<uint8_t>> ty_base(n_chunks);
-  Model N;  // built aside: M is untouched until it is complete
-  for (size_t c = 0; c < n_chunks; ++c) {
-    const LineParser& P = *parsers[c];
-    for (sv x : P.seqids.strs) sq_of[c].push_back(N.seqids.intern(x));
-    for (sv x : P.strands.strs) st_of[c].push_back(N.strands.intern(x));
-    for (sv ft : P.ftypes.strs) {
-      ty_of[c].push_back(N.table(ft));
-      ty_base[c].push_back(ft == "CDS" || ft == "match_part" || ft == "similarity" || ft == "region");
-    }
-  }
-  N.feats.resize(NL);
-  N.ids.strs.resize(NL);
-  N.id_types.resize(NL);
-  N.first_table.resize(NL);
-  N.first_feat.resize(NL);
-  std::vector<Arena> store(n_chunks);
-  if (!par_for(hw, n_chunks, [&](size_t c) {
-        for (size_t k = 0; k < lines[c].size(); ++k) {
-          const GffLine& L = lines[c][k];
-          const uint32_t i = (uint32_t)(base[c] + k);
-          Feature& f = N.feats[i];
-          f.type = ty_of[c][L.ftype];
-          f.seqid = sq_of[c][L.seqid];
-          f.lo = L.lo;
-          f.hi = L.hi;
-          f.strand = st_of[c][L.strand];
-          f.base = ty_base[c][L.ftype] != 0;
-          N.ids.strs[i] = store[c].join({name[i]});
-          N.id_types[i] = 1ull << f.type;
-          N.first_table[i] = (uint8_t)f.type;
-          N.first_feat[i] = i;
-        }
-      }))
-    return false;
-  // parents must not be base features (BaseAnnotation has no child_list)
-  std::vector<uint32_t> n_child(NL, 0);
-  for (uint64_t i = 0; i < NL; ++i)
-    if (parent[i] >= 0) {
-      if (N.feats[(size_t)parent[i]].base) return false;
-      ++n_child[(size_t)parent[i]];
-    }
-  for (uint64_t i = 0; i < NL; ++i)
-    if (n_child[i]) N.feats[i].children.reserve(n_child[i]);
-  std::vector<uint32_t> n_key(N.tables.size(), 0);
-  for (uint64_t i = 0; i < NL; ++i) {
-    if (parent[i] >= 0) N.feats[(size_t)parent[i]].children.push_back((uint32_t)i);
-    ++n_key[N.feats[i].type];
-  }
-  for (size_t t = 0; t < N.tables.size(); ++t) N.tables[t].keys.reserve(n_key[t]);
-  for (uint64_t i = 0; i < NL; ++i) N.tables[N.feats[i].type].keys.push_back((uint32_t)i);
-  for (Arena& ar : store)
-    for (auto& b : ar.blocks) N.ids.chunks.push_back(std::move(b));
-  M = std::move(N);
-  return true;
-}
-
 // read_gff in two passes: the per-line work (columns, tags, IDs, hashes) in
 // parallel over newline-aligned chunks of the text, then the model updates
 // (de-duplication, tables, parents) in file order.  Any diagnostic path
@@ -838,11 +627,6 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
     fprintf(stderr, "[gffplan] parse pass %.3f s (%llu chunks)\n",
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
             (unsigned long long)n_chunks);
-  if (ordered_pass_distinct(M, F, lines, parsers, hw)) {
-    if (std::getenv("MAGOT_GFF_TIMING"))
-      fprintf(stderr, "[gffplan] ordered pass: distinct IDs, in parallel\n");
-    return;
-  }
   uint64_t total = 0;
   for (auto& v : lines) total += v.size();
   M.ids.reserve(total + 16);

@@ -360,35 +360,3 @@ def test_native_from_exons_replace_and_substring_ignore():
                 assert got == want, (kw, seq_type)
                 planned += 1
     assert planned >= 2  # genomic and longest hit the reference's TypeError / ValueError on g2
-
-
-@pytest.mark.parametrize('ids,fast', [('ncbi', True), ('synth', False)])
-@pytest.mark.parametrize('chunks', [None, 5])
-def test_native_plan_parallel_ordered_pass(monkeypatch, capfd, ids, fast, chunks):
-    """read_gff's ordered pass runs in parallel when every final ID is distinct
-    (NCBI-style IDs) and sequentially when renamed IDs meet others (the
-    'synth' IDs: cds5's second part is renamed cds52, transcript 52's CDS);
-    both give the oracle's output, and the same tables."""
-    w = synth.make('small')
-    gff = w.gff3_text(ids=ids)
-    names = list(w.contig_names)
-    lens = [int(x) for x in w.contig_len]
-    if chunks:
-        monkeypatch.setenv('MAGOT_GFF_CHUNKS', str(chunks))
-    monkeypatch.setenv('MAGOT_GFF_TIMING', '1')
-    got = {}
-    for mode in ('default', 'ordered'):
-        if mode == 'ordered':
-            monkeypatch.setenv('MAGOT_GFF_ORDERED', '1')
-        capfd.readouterr()
-        plan = engine.GffPlan.build(gff.encode('latin-1'), names, lens, protein=True,
-                                    order='py2')
-        err = capfd.readouterr().err
-        assert plan is not None
-        got[mode] = (plan.exons.tobytes(), plan.txs.tobytes(), plan.render(
-            *_payloads(plan, [w.contig_bytes(i).tobytes().decode('latin-1')
-                              for i in range(len(names))])))
-        plan.close()
-        if mode == 'default':
-            assert ('distinct IDs, in parallel' in err) == fast
-    assert got['default'] == got['ordered']
