@@ -1,5 +1,6 @@
 #!/bin/bash
-# Tile-count A/B for extract_kernel: MAGOT_EXTRACT_TILE_BYTES caps the tile
+# Tile-count A/B for extract_kernel (apply scripts/experiments/tile_cap.patch
+# first): MAGOT_EXTRACT_TILE_BYTES caps the tile
 # below its slot size, so a plan's tile count lands just under a whole number
 # of resident-wave rounds (6144 waves: 256 CUs x 6 blocks x 4).  One GPU's
 # share of the 4- and 8-GPU jobs and the full C3 job, alternating, two rounds.
