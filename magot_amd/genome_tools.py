@@ -343,13 +343,36 @@ def _flank_native(genome_sequence, gff, sequence_length, stream, feature_type, n
 
 def coords2fasta(fasta_file, seqid, start, stop, truncate_names='False'):
     """genome_tools.py:656-661: header, then contig[start-1:stop] (Python slice
-    rules) gathered on the GPU."""
+    rules) gathered on the GPU.  The FASTA is read and packed natively
+    (magot_genome_load_fasta) unless a header needs the Python reader."""
     _write('>' + seqid + ':' + start + '-' + stop + '\n')
-    seqs = genome.Genome(fasta_file, truncate_names=_literal(truncate_names)).genome_sequence
-    contig = seqs[seqid]
-    st, ln = genome._slice_interval(contig, int(start) - 1, int(stop))
-    index = {name: i for i, name in enumerate(seqs)}
-    _write(_gather(seqs, [(index[seqid], st, ln, False)])[0] + '\n')
+    truncate = _literal(truncate_names)
+    dev = None
+    if isinstance(truncate, bool):
+        dev = engine.FastaGenome.load(genome.read_buffer(fasta_file), truncate_names=truncate)
+    if dev is None:
+        seqs = genome.Genome(fasta_file, truncate_names=truncate).genome_sequence
+        contig = seqs[seqid]
+        st, ln = genome._slice_interval(contig, int(start) - 1, int(stop))
+        index = {name: i for i, name in enumerate(seqs)}
+        _write(_gather(seqs, [(index[seqid], st, ln, False)])[0] + '\n')
+        return
+    c = dev.index[seqid]  # KeyError, as genome_sequence[seqid]
+    a, b = slice(int(start) - 1, int(stop)).indices(int(dev.lengths[c]))[:2]
+    _write_bytes(_gather_device(dev, [(c, a, max(0, b - a), False)])[0], b'\n')
+
+
+def _gather_device(dev, intervals):
+    """Bytes of (contig index, start, length, rc) intervals on a device
+    genome: one kernel launch."""
+    ex = np.zeros(len(intervals), dtype=engine.EXON_DTYPE)
+    for i, (c, st, ln, rc) in enumerate(intervals):
+        ex[i] = ((st | (1 << 63)) if rc else st, c, ln)
+    tx = np.zeros(len(intervals), dtype=engine.TX_DTYPE)
+    tx['exon_begin'] = np.arange(len(intervals))
+    tx['n_exons'] = 1
+    nuc, noff, _, _ = engine.extract_records(dev, ex, tx, engine.OUT_NUC)
+    return [nuc[int(noff[i]):int(noff[i + 1])].tobytes() for i in range(len(intervals))]
 
 
 def _match_fasta(g, order):

@@ -107,3 +107,25 @@ def test_gpu_coords2fasta_matches_reference(small, key):
     text, exc = _run_cli(genome_tools.coords2fasta, small[0], seqid, a, b, tr)
     assert exc == GOLD[key]['exc']
     assert text == GOLD[key]['stdout']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('tr', ['True', 'False'])
+def test_gpu_coords2fasta_native_load(monkeypatch, tr):
+    """coords2fasta on the O.biroi FASTA: read and packed natively
+    (FastaGenome.load, never the Python reader), windows across the contig
+    ends and Python slice rules, against the oracle."""
+    from magot_amd import genome, genome_tools
+    monkeypatch.setattr(genome.Genome, '__init__', lambda *a, **k: (_ for _ in ()).throw(
+        AssertionError('the Python FASTA reader ran')))
+    fa = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
+    seqs = mo.read_fasta(fa, truncate_names=tr == 'True')
+    name = sorted(seqs, key=lambda k: -len(seqs[k]))[0]
+    L = len(seqs[name])
+    for a, b in ((1, 100), (0, 10), (-5, 20), (L - 50, L + 50), (500, 400), (1, L)):
+        want, exc = mo.coords2fasta(fa, name, str(a), str(b), tr)
+        assert exc is None
+        text, exc = _run_cli(genome_tools.coords2fasta, fa, name, str(a), str(b), tr)
+        assert exc is None and text == want
+    text, exc = _run_cli(genome_tools.coords2fasta, fa, 'no-such-contig', '1', '5', tr)
+    assert exc == 'KeyError' and text == '>no-such-contig:1-5\n'
