@@ -293,15 +293,19 @@ def extract_upstream_downstream(genome_sequence, gff, sequence_length, stream,
                         name = attribute.split('=')[1].replace('\r', '').replace('\n', '')
                 if name is None:
                     name = 'seq' + str(len(items))
+                # evaluation order of the reference: the contig (KeyError),
+                # then int(sequence_length) (ValueError)
                 if stream == 'up' and fields[6] == '+' or stream == 'down' and fields[6] == '-':
                     stop = coords[0] - 1
+                    contig = seqs[fields[0]]
                     n = int(sequence_length)
-                    st, ln = genome._slice_interval(seqs[fields[0]], stop - n, stop)
+                    st, ln = genome._slice_interval(contig, stop - n, stop)
                     current = (index[fields[0]], st, ln, False)
                 elif stream == 'down' and fields[6] == '+' or stream == 'up' and fields[6] == '-':
                     start = coords[1]
+                    contig = seqs[fields[0]]
                     n = int(sequence_length)
-                    st, ln = genome._slice_interval(seqs[fields[0]], start, start + n)
+                    st, ln = genome._slice_interval(contig, start, start + n)
                     current = (index[fields[0]], st, ln, True)
                 if current is None:
                     raise UnboundLocalError(

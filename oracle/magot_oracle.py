@@ -653,19 +653,21 @@ def extract_upstream_downstream(genome_sequence, gff_path, sequence_length, stre
                         name = attribute.split('=')[1].replace('\r', '').replace('\n', '')
                 if name is None:
                     name = 'seq' + str(len(output_seqs))
-                n = int(sequence_length)
+                # int(sequence_length) where the reference evaluates it: in a
+                # branch, then in the comparison (after the unbound check)
                 if stream == 'up' and fields[6] == '+' or stream == 'down' and fields[6] == '-':
                     stop = coords[0] - 1
-                    sequence = seqs[fields[0]][stop - n:stop]
+                    sequence = seqs[fields[0]][stop - int(sequence_length):stop]
                     bound = True
                 elif stream == 'down' and fields[6] == '+' or stream == 'up' and fields[6] == '-':
                     start = coords[1]
-                    sequence = reverse_complement(seqs[fields[0]][start:start + n])
+                    sequence = reverse_complement(
+                        seqs[fields[0]][start:start + int(sequence_length)])
                     bound = True
                 if not bound:
                     raise UnboundLocalError("local variable 'sequence' referenced before "
                                             "assignment")
-                if len(sequence) == n:
+                if len(sequence) == int(sequence_length):
                     output_seqs.append('>' + name + '\n' + sequence)
     return '\n'.join(output_seqs) + '\n'
 

@@ -15,11 +15,12 @@ Outputs (data only: inputs, expected outputs, hashes):
   fixtures.json   hashes of whole-file gff2fasta outputs on the shipped data
   synth_small.json hashes of gff2fasta on the seeded small synthetic
   loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
+  flank_edges.json extract_upstream_downstream on the native flank planner's edge cases
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
   translate_lib.json Sequence.translate with non-standard libraries, frames -6..6
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges]
 """
 
 import contextlib
@@ -300,6 +301,67 @@ LOCUS_GFF = ''.join([
     'c2\tt\tmRNA\t12\t20\t.\t+\t.\tID=m4;Parent=g4\n',
     'c2\tt\tgene\t2\t5\t.\t+\t.\tID=g5\n',
 ])
+
+
+FLANK_GENOME = '>c1 first contig\n' + 'ACGTTGCAACGGATCC' * 8 + '\n>c2\n' + 'TTAGGCAT' * 6 + '\n'
+FLANK_CASES = [
+    # (gff text, sequence_length, stream, feature_type, namefrom)
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a\nc1\tt\tgene\t60\t70\t.\t.\t.\tID=b\n'
+     'c1\tt\tgene\t80\t90\t.\t?\t.\tName=z\n', '5', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t-\t.\tID=a\nc1\tt\tgene\t60\t70\t.\t+\n', '5', 'down',
+     'gene', 'ID'),
+    ('c1\tt\tgene\t1\t9\t.\t+\t.\tID=a\nc1\tt\tgene\t0\t9\t.\t+\t.\tID=b\n'
+     'c2\tt\tgene\t40\t48\t.\t+\t.\tID=c\nc2\tt\tgene\t2\t47\t.\t-\t.\tID=d\n', '4', 'up',
+     'gene', 'ID'),
+    ('c1\tt\tgene\t1\t9\t.\t+\t.\tID=a\nc1\tt\tgene\t0\t9\t.\t+\t.\tID=b\n'
+     'c2\tt\tgene\t40\t48\t.\t+\t.\tID=c\nc2\tt\tgene\t2\t47\t.\t-\t.\tID=d\n', '4', 'down',
+     'gene', 'ID'),
+    ('#c1\tt\tgene\t5\t9\t.\t+\t.\tID=hidden\r\n'
+     'c1\tt\tgene\t30\t20\t.\t+\t.\tID=x=y;Name=n; ID=no;ID=last\r\n'
+     'c2\tt\tgene\t20\t30\t.\t-\t.\tName=q\r\n', '6', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a\nc2\tt\tgene\t10\t12\t.\t-\t.\n', '0', 'up',
+     'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a\n', '-3', 'down', 'gene', 'ID'),
+    ('c1\tt\tmRNA\t40\t50\t.\t+\t.\tID=a\n', '5', 'up', 'gene', 'ID'),
+    ('', '5', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a\nnope\tt\tgene\t60\t70\t.\t.\t.\tID=b\n', '5',
+     'up', 'gene', 'ID'),
+    ('', '5', 'sideways', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tName=a;Name=b=c;gene=g\n', '7', 'down', 'gene', 'Name'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a;\n', '5', 'up', 'gene', ''),
+    ('c1\tt\tgene\t40\t50\t.\t.\t.\tID=a\n', '5', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a\n', '5', 'sideways', 'gene', 'ID'),
+    ('nope\tt\tgene\t40\t50\t.\t+\t.\tID=a\n', '5', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t4x\t50\t.\t+\t.\tID=a\n', '5', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID;Name=a\n', '5', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a\n', 'five', 'up', 'gene', 'ID'),
+    ('c1\tt\tgene\t40\t50\t.\t+\t.\tID=a\n', 'five', 'sideways', 'gene', 'ID'),
+    ('nope\tt\tgene\t40\t50\t.\t+\t.\tID=a\n', 'five', 'up', 'gene', 'ID'),
+]
+
+
+def make_flank_edges(ref):
+    """The reference's extract_upstream_downstream (:457-480) on the edge cases
+    of the native flank planner (tests/test_flank.py): stdout and exception.
+    No case ends a line with a lone '\\r' (Python 3's universal newlines would
+    split there, Python 2's file iteration does not)."""
+    sys.path.insert(0, PY3)
+    import genome_tools as rt
+    import tempfile
+    cases = []
+    with tempfile.TemporaryDirectory() as td:
+        fa_path = os.path.join(td, 'g.fa')
+        with open(fa_path, 'w') as fh:
+            fh.write(FLANK_GENOME)
+        for k, (gff, n, stream, ft, nf) in enumerate(FLANK_CASES):
+            gff_path = os.path.join(td, 'a%d.gff' % k)
+            with open(gff_path, 'w', newline='') as fh:
+                fh.write(gff)
+            _, exc, so = call(lambda: rt.extract_upstream_downstream(fa_path, gff_path, n, stream,
+                                                                    ft, nf, 'True'))
+            cases.append({'gff': gff, 'sequence_length': n, 'stream': stream,
+                          'feature_type': ft, 'namefrom': nf, 'stdout': so, 'exc': exc})
+    return {'genome': FLANK_GENOME, 'cases': cases}
 
 
 def make_locus(ref):
@@ -695,6 +757,10 @@ def main():
         json.dump(make_translate_lib(ref), fh, indent=0, sort_keys=True)
     if '--only-translate-lib' in sys.argv:
         return
+    if '--only-flank-edges' in sys.argv:
+        with open(os.path.join(HERE, 'flank_edges.json'), 'w') as fh:
+            json.dump(make_flank_edges(ref), fh, indent=1, sort_keys=True)
+        return
     with open(os.path.join(HERE, 'fuzz.json'), 'w') as fh:
         json.dump(make_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'fuzz2.json'), 'w') as fh:
@@ -706,6 +772,8 @@ def main():
         json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:
         json.dump(make_locus(ref), fh, indent=1, sort_keys=True)
+    with open(os.path.join(HERE, 'flank_edges.json'), 'w') as fh:
+        json.dump(make_flank_edges(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'kat.json'), 'w') as fh:
         json.dump(make_kat(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'edge_cases.json'), 'w') as fh:

@@ -151,6 +151,34 @@ def test_native_flank_declines_error_paths(tmp_path, gff, args):
     assert native_flank(str(fa), str(gf), *args) is None
 
 
+EDGES = json.load(open(os.path.join(goldlib.HERE, 'flank_edges.json')))
+
+
+def _edge_files(tmp_path, case):
+    fa, gf = tmp_path / 'g.fa', tmp_path / 'a.gff'
+    fa.write_text(EDGES['genome'])
+    gf.write_bytes(case['gff'].encode('latin-1'))
+    return str(fa), str(gf), (case['sequence_length'], case['stream'], case['feature_type'],
+                              case['namefrom'])
+
+
+@pytest.mark.parametrize('k', range(len(EDGES['cases'])))
+def test_flank_edges_match_reference(tmp_path, k):
+    """tests/golden/flank_edges.json: the REFERENCE's stdout / exception on the
+    edge cases (make_golden.py --only-flank-edges).  The oracle reproduces
+    them; the native planner renders the same text or declines exactly where
+    the reference raises."""
+    case = EDGES['cases'][k]
+    fa, gf, args = _edge_files(tmp_path, case)
+    want, exc = _oracle(fa, gf, *args)
+    assert exc == case['exc']
+    if exc is None:
+        assert want == case['stdout']
+        assert native_flank(fa, gf, *args) == case['stdout']
+    else:
+        assert native_flank(fa, gf, *args) is None
+
+
 # ---------------------------------------------------------------------------
 # GPU: the drop-in CLI function on the native path (windows gathered by the
 # extraction kernel, text assembled on the device) against the oracle
@@ -209,3 +237,17 @@ def test_gpu_flank_edges_and_declines(tmp_path):
     gf.write_text('c1\tt\tgene\t40\t50\t.\t.\t.\tID=a\n')
     with pytest.raises(UnboundLocalError):
         _cli(str(fa), str(gf), '5', 'up')
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('k', range(len(EDGES['cases'])))
+def test_gpu_flank_edges_match_reference(tmp_path, k):
+    case = EDGES['cases'][k]
+    fa, gf, args = _edge_files(tmp_path, case)
+    try:
+        text, exc = _cli(fa, gf, *args), None
+    except Exception as e:  # noqa: BLE001
+        text, exc = None, type(e).__name__
+    assert exc == case['exc']
+    if exc is None:
+        assert text == case['stdout']
