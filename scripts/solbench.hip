@@ -22,7 +22,8 @@
 // c5 chain: the same stores after 1, 3 or 5 dependent load round trips per
 //     wave (staging's shape), with loads and stores in the same or in
 //     separate waves, and with extra load instructions per round.
-//   usage: solbench c3 | solbench c5 [chain]
+// c5 now: the chain over round 4's layout and block order.
+//   usage: solbench c3 | solbench c5 [chain | now]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -148,11 +149,16 @@ __global__ __launch_bounds__(256) void c5_replay(C5Args a) {
 // waves only store (their partner's runs too): loads never queue behind the
 // same wave's stores (a producer / consumer split of the staging and chunk
 // phases, without the hand-off).
-template <bool kSplit>
+// kNow: orf6_kernel as of round 4 -- blocks in the hardware's round-robin
+// XCD order and the records' blocks laid out in walk order (tile w's runs
+// follow tile w-1's)
+// kRr: the hardware's round-robin block order (else one contiguous run of
+// tiles per XCD)
+template <bool kSplit, bool kNow = false, bool kRr = kNow>
 __global__ __launch_bounds__(256) void c5_chain(C5Args a, uint32_t chain, uint32_t extra) {
   const uint32_t xnb = gridDim.x, xb = blockIdx.x;
   const uint32_t xq = xnb >> 3, xr = xnb & 7, xcd = xb & 7, xk = xb >> 3;
-  const uint32_t vb = xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
+  const uint32_t vb = kRr ? xb : xcd < xr ? xcd * (xq + 1) + xk : xr * (xq + 1) + (xcd - xr) * xq + xk;
   const uint64_t w = (uint64_t)vb * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (w >= a.ntiles) return;
@@ -182,7 +188,8 @@ __global__ __launch_bounds__(256) void c5_chain(C5Args a, uint32_t chain, uint32
     const uint64_t wr = (uint64_t)a.win_tiles * a.runs;
     for (uint32_t q = lane; q < total; q += 64) {
       const uint32_t r = q / per, c = q - r * per;
-      const uint64_t slot = ((w / a.win_tiles) * wr + mix(w * 64 + r) % wr) % a.out_runs;
+      const uint64_t slot = kNow ? (w * runs + r) % a.out_runs
+                                 : ((w / a.win_tiles) * wr + mix(w * 64 + r) % wr) % a.out_runs;
       st16(a.out + slot * a.run_bytes + 16 * c, make_uint4(acc, q, r, (uint32_t)w), false);
     }
   }
@@ -296,6 +303,35 @@ int main(int argc, char** argv) {
     }
     timeit([&] { hipLaunchKernelGGL((c5_replay<false, false>), grid, 256, pad, 0, a); },
            "c5 replay: 21 fills, scattered, buffer 1 again", wb, rb);
+    if (argc > 2 && !strcmp(argv[2], "now")) {
+      // round 4's orf6: walk-order layout, round-robin blocks, 2.00 GB of
+      // fills per launch (profiles/r04_close/traffic_C5: ~26 lines per tile)
+      const uint32_t l4 = 26;
+      C5Args b{pl, plane / 128, o, out / run, ntiles, l4, run, runs, sink, 3000u};
+      const double rb4 = (double)ntiles * l4 * 128;
+      const size_t padc = lds_pad(reinterpret_cast<const void*>(c5_chain<false, true>), 7);
+      for (uint32_t chain : {1u, 3u, 5u}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "c5 now: %u dependent load rounds", chain);
+        timeit([&] { hipLaunchKernelGGL((c5_chain<false, true>), grid, 256, padc, 0, b, chain, 0u); },
+               nm, wb, rb4);
+      }
+      C5Args z{pl, plane / 128, o, out / run, ntiles, 0u, run, runs, sink, 3000u};
+      timeit([&] { hipLaunchKernelGGL((c5_chain<false, true>), grid, 256, padc, 0, z, 1u, 0u); },
+             "c5 now: stores only", wb, 0.0);
+      timeit([&] { hipLaunchKernelGGL((c5_chain<true, true>), grid, 256, padc, 0, b, 5u, 0u); },
+             "c5 now: 5 rounds, load/store waves split", wb, rb4);
+      // the same walk-order layout with one contiguous run of tiles per XCD
+      // (round 3's order: 1.64 GB of fills, ~21 lines per tile)
+      C5Args c{pl, plane / 128, o, out / run, ntiles, 21u, run, runs, sink, 3000u};
+      timeit([&] { hipLaunchKernelGGL((c5_chain<false, true, false>), grid, 256, padc, 0, c, 5u, 0u); },
+             "c5 now, XCD runs, 21 fills: 5 rounds", wb, (double)ntiles * 21 * 128);
+      timeit([&] { hipLaunchKernelGGL((c5_chain<false, true, true>), grid, 256, padc, 0, c, 5u, 0u); },
+             "c5 now, round-robin, 21 fills: 5 rounds", wb, (double)ntiles * 21 * 128);
+      timeit([&] { hipLaunchKernelGGL((c5_chain<false, true, false>), grid, 256, padc, 0, z, 1u, 0u); },
+             "c5 now, XCD runs: stores only", wb, 0.0);
+      return 0;
+    }
     if (argc > 2 && !strcmp(argv[2], "chain")) {
       C5Args b{pl, plane / 128, o, out / run, ntiles, 21u, run, runs, sink, 3000u};
       const size_t padc = lds_pad(reinterpret_cast<const void*>(c5_chain<false>), 7);
