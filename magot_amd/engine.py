@@ -281,25 +281,47 @@ def extract_records(genome, exons, txs, outputs=OUT_NUC | OUT_PEP):
     return nuc, noff, pep, poff
 
 
-def fasta_read(text, truncate_names=False):
-    """Native GenomeSequence reader (magot_fasta_read): [(name, bytes)], or None
-    when a header needs the Python reader.  Host only."""
-    L = _lib.lib()
-    data = _text_view(text)
-    tp = _text_ptr(data)
+def _fasta_index(L, tp, size, truncate_names):
+    """(count, lengths, NUL-separated name bytes) of a FASTA text, or None."""
     n = ctypes.c_uint32()
     nl = ctypes.c_uint64()
-    rc = L.magot_fasta_read(tp, len(data), int(bool(truncate_names)), ctypes.byref(n), None,
+    rc = L.magot_fasta_read(tp, size, int(bool(truncate_names)), ctypes.byref(n), None,
                             None, 0, ctypes.byref(nl), None, 0)
     if rc == _lib.ERR_UNSUPPORTED:
         return None
     check(rc, 'magot_fasta_read')
     lens = np.zeros(max(n.value, 1), dtype=np.uint64)
     names = np.zeros(max(nl.value, 1), dtype=np.uint8)
-    seqs = np.zeros(max(int(lens.sum()), 1), dtype=np.uint8)
-    check(L.magot_fasta_read(tp, len(data), int(bool(truncate_names)), ctypes.byref(n),
+    check(L.magot_fasta_read(tp, size, int(bool(truncate_names)), ctypes.byref(n),
                              ptr(lens), ptr(names), nl.value, ctypes.byref(nl), None, 0),
           'magot_fasta_read')
+    return n, lens, names, nl
+
+
+def fasta_contigs(text, truncate_names=False):
+    """(names, lengths) of the contigs the native reader (magot_fasta_read)
+    finds in a FASTA text, without copying any sequence; None when a header
+    needs the Python reader.  Host only."""
+    L = _lib.lib()
+    data = _text_view(text)
+    idx = _fasta_index(L, _text_ptr(data), len(data), truncate_names)
+    if idx is None:
+        return None
+    n, lens, names, nl = idx
+    nms = names[:nl.value].tobytes().split(b'\0')[:n.value]
+    return [x.decode('latin-1') for x in nms], [int(x) for x in lens[:n.value]]
+
+
+def fasta_read(text, truncate_names=False):
+    """Native GenomeSequence reader (magot_fasta_read): [(name, bytes)], or None
+    when a header needs the Python reader.  Host only."""
+    L = _lib.lib()
+    data = _text_view(text)
+    tp = _text_ptr(data)
+    idx = _fasta_index(L, tp, len(data), truncate_names)
+    if idx is None:
+        return None
+    n, lens, names, nl = idx
     seqs = np.zeros(max(int(lens[:n.value].sum()), 1), dtype=np.uint8)
     check(L.magot_fasta_read(tp, len(data), int(bool(truncate_names)), ctypes.byref(n),
                              ptr(lens), ptr(names), nl.value, ctypes.byref(nl), ptr(seqs),

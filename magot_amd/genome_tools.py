@@ -97,8 +97,33 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
     object path to reuse."""
     if order not in ('py2', 'insertion'):
         raise ValueError("order must be 'insertion' or 'py2'")
-    # the FASTA is read and packed natively; Python reader for unusual headers
-    dev = engine.FastaGenome.load(genome.read_buffer(genome_sequence))
+    protein = seq_type == 'protein'
+
+    def plan_gff(names, lengths):
+        return engine.GffPlan.build(genome.read_buffer(gff), names, lengths, protein=protein,
+                                    order=order, longest=longest, genomic=genomic,
+                                    from_exons=from_exons)
+
+    # the FASTA is read and packed natively; Python reader for unusual headers.
+    # The GFF needs only the contig names and lengths (a host scan of the
+    # FASTA), so it is planned while another thread starts the device and
+    # uploads and packs the genome (both native calls release the GIL).
+    fa = genome.read_buffer(genome_sequence)
+    index = engine.fasta_contigs(fa)
+    dev = plan = None
+    if index is not None:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(1) as pool:
+            loading = pool.submit(engine.FastaGenome.load, fa)
+            try:
+                plan = plan_gff(*index)
+            finally:
+                dev = loading.result()
+        if dev is None and plan is not None:  # above one device plane
+            plan.close()
+            plan = None
+        elif dev is not None and plan is None:
+            return None, None
     seqs = None
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)
@@ -107,13 +132,9 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
             # decided before anything is packed
             return None, seqs
         dev = seqs.device()
-    names = dev.names
-    protein = seq_type == 'protein'
-    plan = engine.GffPlan.build(genome.read_buffer(gff), names, [int(x) for x in dev.lengths],
-                                protein=protein, order=order, longest=longest, genomic=genomic,
-                                from_exons=from_exons)
-    if plan is None:
-        return None, seqs
+        plan = plan_gff(dev.names, [int(x) for x in dev.lengths])
+        if plan is None:
+            return None, seqs
     try:
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                    engine.OUT_PEP if plan.protein else engine.OUT_NUC)
