@@ -108,22 +108,22 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
     # The GFF needs only the contig names and lengths (a host scan of the
     # FASTA), so it is planned while another thread starts the device and
     # uploads and packs the genome (both native calls release the GIL).
+    from concurrent.futures import ThreadPoolExecutor
     fa = genome.read_buffer(genome_sequence)
-    index = engine.fasta_contigs(fa)
-    dev = plan = None
-    if index is not None:
-        from concurrent.futures import ThreadPoolExecutor
-        with ThreadPoolExecutor(1) as pool:
-            loading = pool.submit(engine.FastaGenome.load, fa)
-            try:
+    with ThreadPoolExecutor(1) as pool:
+        loading = pool.submit(engine.FastaGenome.load, fa)
+        plan = None
+        try:
+            index = engine.fasta_contigs(fa)  # the same reader as the load
+            if index is not None:
                 plan = plan_gff(*index)
-            finally:
-                dev = loading.result()
-        if dev is None and plan is not None:  # above one device plane
-            plan.close()
-            plan = None
-        elif dev is not None and plan is None:
-            return None, None
+        finally:
+            dev = loading.result()
+    if dev is None and plan is not None:  # above one device plane
+        plan.close()
+        plan = None
+    elif dev is not None and plan is None:
+        return None, None
     seqs = None
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)
