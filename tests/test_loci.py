@@ -129,3 +129,28 @@ def test_gpu_coords2fasta_native_load(monkeypatch, tr):
         assert exc is None and text == want
     text, exc = _run_cli(genome_tools.coords2fasta, fa, 'no-such-contig', '1', '5', tr)
     assert exc == 'KeyError' and text == '>no-such-contig:1-5\n'
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('seed', range(40))
+def test_gpu_coords2fasta_random(seed):
+    """Seeded random windows on the O.biroi contigs (Python slice rules:
+    starts at or below 0, stops past the end, empty and reversed windows,
+    malformed numbers) through the native coords2fasta, against the oracle."""
+    import random
+
+    from magot_amd import genome_tools
+    rnd = random.Random(seed)
+    fa = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
+    tr = rnd.choice(['True', 'False'])
+    seqs = mo.read_fasta(fa, truncate_names=tr == 'True')
+    name = rnd.choice(sorted(seqs) + ['absent'])
+    L = len(seqs.get(name, 'x' * 1000))
+    pick = lambda: str(rnd.choice([rnd.randint(-L - 10, L + 10), 0, 1, L, L + 1, -1]))
+    a, b = pick(), pick()
+    if rnd.random() < 0.05:
+        b = '12x'
+    want, exc = mo.coords2fasta(fa, name, a, b, tr)
+    text, gexc = _run_cli(genome_tools.coords2fasta, fa, name, a, b, tr)
+    assert gexc == (type(exc).__name__ if exc else None)
+    assert text == want
