@@ -444,6 +444,33 @@ def test_c5_full_size_six_frames_vs_c_oracle():
     assert cds_oracle.orf6_compare(ref, roff, out, soff, slen, threads=threads) == (0, -1)
 
 
+@pytest.mark.parametrize('seed', [7, 8])
+def test_huge_exons_vs_c_oracle(seed):
+    """Records far larger than a tile: 15 % of the exons 20-300 kb (clamped at
+    the contig ends as Python slices are), so one record spans dozens of
+    extraction tiles and orf6 windows, its peptide and six streams continue
+    across every tile boundary; extraction and all six frames against the C
+    oracle."""
+    from oracle import cds_oracle
+    rng = np.random.default_rng(seed)
+    w = synth.make('small', seed=seed, genome_bases=3_000_000, n_tx=150, iupac_rate=1e-3)
+    big = rng.random(w.n_exons) < 0.15
+    w.ex_len = np.where(big, rng.integers(20_000, 300_000, size=w.n_exons), w.ex_len)
+    check_against_oracle(w)
+    dev = engine.DeviceGenome(w.contigs())
+    ex, tx = w.plan_tables()
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC)
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    o6.close()
+    plan.close()
+    dev.close()
+    ref, roff, st = cds_oracle.extract_workload(w, False)
+    assert not st.any() and int(roff[-1]) > 10 * 5072
+    assert cds_oracle.orf6_compare(ref, roff, out, soff, slen, threads=4) == (0, -1)
+
+
 @pytest.mark.parametrize('paths', ['1', '2', '3'])
 def test_forced_general_paths_vs_c_oracle(monkeypatch, paths):
     """MAGOT_DEBUG_PATHS routes every chunk (1), every residue chunk (2) or
