@@ -531,6 +531,50 @@ def test_degenerate_intervals_vs_c_oracle():
     check_against_oracle(w)
 
 
+@pytest.mark.parametrize('shape', ['no_records', 'all_empty', 'one_base_each'])
+def test_empty_and_tiny_plans(shape):
+    """Plans with no record, with records whose intervals are all empty, and
+    with one-base records: extraction, translation and the six-frame plan
+    return empty or exact outputs without launching out of range."""
+    w = synth.make('small', seed=3, genome_bases=200_000, n_tx=50)
+    dev = engine.DeviceGenome(w.contigs())
+    ex, tx = w.plan_tables()
+    if shape == 'no_records':
+        ex, tx = ex[:0], tx[:0]
+    elif shape == 'all_empty':
+        ex['len'] = 0
+    else:
+        ex['len'] = np.minimum(ex['len'], 1)
+        tx['n_exons'] = np.minimum(tx['n_exons'], 1)
+        ex = ex[tx['exon_begin'].astype(np.int64)]
+        tx['exon_begin'] = np.arange(len(tx))
+    plan = engine.ExtractionPlan(dev, ex, tx, engine.OUT_NUC | engine.OUT_PEP)
+    nuc, noff, pep, poff = plan.run()
+    lens = ex['len'].astype(np.int64)
+    assert len(noff) == len(tx) + 1 and int(noff[-1]) == int(lens.sum())
+    assert int(poff[-1]) == 0  # no record reaches one codon
+    if shape == 'one_base_each':
+        seqs = [s for _, s in w.contigs()]
+        for r in range(len(tx)):
+            st = int(ex['start_rc'][r]) & ((1 << 63) - 1)
+            b = seqs[int(ex['contig'][r])][st:st + int(ex['len'][r])]
+            if int(ex['start_rc'][r]) >> 63:
+                b = mo_revcomp(b)
+            assert nuc[int(noff[r]):int(noff[r + 1])].tobytes() == b
+    o6 = engine.Orf6Plan(plan)
+    o6.execute()
+    out, soff, slen = o6.fetch()
+    assert len(soff) == 6 * len(tx) + 1 and not slen.any()
+    o6.close()
+    plan.close()
+    dev.close()
+
+
+def mo_revcomp(b):
+    from oracle import magot_oracle as mo
+    return mo.reverse_complement(b.decode('latin-1')).encode('latin-1')
+
+
 # ---------------------------------------------------------------------------
 # Six-frame translation (Sequence.get_orfs, genome.py:824-851): orf6_kernel
 # ---------------------------------------------------------------------------
