@@ -18,9 +18,11 @@ Outputs (data only: inputs, expected outputs, hashes):
   flank_edges.json extract_upstream_downstream on the native flank planner's edge cases
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
+  fuzz3.json      200 more of them (another seed)
   translate_lib.json Sequence.translate with non-standard libraries, frames -6..6
 
-Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges]
+Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges |
+                                           --only-fuzz3]
 """
 
 import contextlib
@@ -631,10 +633,11 @@ FUZZ_CALLS = [('nucleotide', False, 'insertion'), ('protein', False, 'insertion'
               ('protein', False, 'py2')]
 
 
-def make_fuzz(ref, n=60):
+def make_fuzz(ref, n=60, seed=20261016):
     """Random small annotation sets through the reference's gff2fasta path
-    (Genome + read_gff + get_fasta, tests/test_fuzz.py)."""
-    rnd = random.Random(20261016)
+    (Genome + read_gff + get_fasta, tests/test_fuzz.py).  fuzz3.json: 200 more
+    from seed 20261017."""
+    rnd = random.Random(seed)
     out = []
     for i in range(n):
         fasta, gff = _fuzz_case(rnd)
@@ -757,6 +760,10 @@ def main():
         json.dump(make_translate_lib(ref), fh, indent=0, sort_keys=True)
     if '--only-translate-lib' in sys.argv:
         return
+    if '--only-fuzz3' in sys.argv:
+        with open(os.path.join(HERE, 'fuzz3.json'), 'w') as fh:
+            json.dump(make_fuzz(ref, n=200, seed=20261017), fh, indent=0, sort_keys=True)
+        return
     if '--only-flank-edges' in sys.argv:
         with open(os.path.join(HERE, 'flank_edges.json'), 'w') as fh:
             json.dump(make_flank_edges(ref), fh, indent=1, sort_keys=True)
@@ -765,6 +772,8 @@ def main():
         json.dump(make_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'fuzz2.json'), 'w') as fh:
         json.dump(make_fuzz2(ref), fh, indent=0, sort_keys=True)
+    with open(os.path.join(HERE, 'fuzz3.json'), 'w') as fh:
+        json.dump(make_fuzz(ref, n=200, seed=20261017), fh, indent=0, sort_keys=True)
     import genome_tools as ref_tools  # the reference's, from the same Python 3 copy
     with open(os.path.join(HERE, 'cds2pep.json'), 'w') as fh:
         json.dump(make_cds2pep(ref_tools), fh, indent=0, sort_keys=True)

@@ -1,5 +1,5 @@
-"""Randomised gff2fasta cases against the REFERENCE (tests/golden/fuzz.json and
-fuzz2.json,
+"""Randomised gff2fasta cases against the REFERENCE (tests/golden/fuzz.json,
+fuzz3.json and fuzz2.json,
 made by tests/golden/make_golden.py from the reference's own Genome /
 read_gff / get_fasta): small genomes with lower case, N and IUPAC bytes, and
 GFF3 / GTF files with renamed duplicate IDs, reversed, zero and past-end
@@ -22,7 +22,9 @@ import pytest
 import goldlib
 from oracle import magot_oracle as mo
 
-CASES = json.load(open(os.path.join(goldlib.HERE, 'fuzz.json')))
+# fuzz3.json: 200 more cases of the same generator, another seed
+CASES = json.load(open(os.path.join(goldlib.HERE, 'fuzz.json'))) + \
+    json.load(open(os.path.join(goldlib.HERE, 'fuzz3.json')))
 # genomic=True, longest protein and from_exons=True (exon features as CDS)
 CASES2 = json.load(open(os.path.join(goldlib.HERE, 'fuzz2.json')))
 
