@@ -22,7 +22,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   translate_lib.json Sequence.translate with non-standard libraries, frames -6..6
 
 Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges |
-                                           --only-fuzz3]
+                                           --only-fuzz3 | --only-cds2pep2]
 """
 
 import contextlib
@@ -737,11 +737,12 @@ def _cds_case(rnd):
     return text
 
 
-def make_cds2pep(ref_tools, n=40):
+def make_cds2pep(ref_tools, n=40, seed=20261018):
     """genome_tools.cds2pep (:664-675) on random FASTA files: its stdout and
-    exception (tests/test_cds2pep.py)."""
+    exception (tests/test_cds2pep.py).  cds2pep2.json: 160 more from seed
+    20261019."""
     import tempfile
-    rnd = random.Random(20261018)
+    rnd = random.Random(seed)
     out = []
     with tempfile.TemporaryDirectory() as d:
         for i in range(n):
@@ -760,6 +761,12 @@ def main():
         json.dump(make_translate_lib(ref), fh, indent=0, sort_keys=True)
     if '--only-translate-lib' in sys.argv:
         return
+    if '--only-cds2pep2' in sys.argv:
+        sys.path.insert(0, PY3)
+        import genome_tools as ref_tools
+        with open(os.path.join(HERE, 'cds2pep2.json'), 'w') as fh:
+            json.dump(make_cds2pep(ref_tools, n=160, seed=20261019), fh, indent=0, sort_keys=True)
+        return
     if '--only-fuzz3' in sys.argv:
         with open(os.path.join(HERE, 'fuzz3.json'), 'w') as fh:
             json.dump(make_fuzz(ref, n=200, seed=20261017), fh, indent=0, sort_keys=True)
@@ -777,6 +784,8 @@ def main():
     import genome_tools as ref_tools  # the reference's, from the same Python 3 copy
     with open(os.path.join(HERE, 'cds2pep.json'), 'w') as fh:
         json.dump(make_cds2pep(ref_tools), fh, indent=0, sort_keys=True)
+    with open(os.path.join(HERE, 'cds2pep2.json'), 'w') as fh:
+        json.dump(make_cds2pep(ref_tools, n=160, seed=20261019), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'matches.json'), 'w') as fh:
         json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:

@@ -18,7 +18,9 @@ import pytest
 import goldlib
 from oracle import magot_oracle as mo
 
-CASES = json.load(open(os.path.join(goldlib.HERE, 'cds2pep.json')))
+# cds2pep2.json: 160 more cases of the same generator, another seed
+CASES = json.load(open(os.path.join(goldlib.HERE, 'cds2pep.json'))) + \
+    json.load(open(os.path.join(goldlib.HERE, 'cds2pep2.json')))
 
 
 def _write_case(tmp_path, i):
