@@ -19,6 +19,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
   fuzz3.json      200 more of them (another seed)
+  fuzz4.json      120 more cases of fuzz2.json's generator (another seed)
   translate_lib.json Sequence.translate with non-standard libraries, frames -6..6
 
 Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges |
@@ -689,11 +690,12 @@ FUZZ2_CALLS = [('nucleotide', False, True, False, 'insertion'), ('protein', Fals
                ('nucleotide', True, False, True, 'insertion')]
 
 
-def make_fuzz2(ref, n=40):
+def make_fuzz2(ref, n=40, seed=20261017):
     """The gff2fasta options fuzz.json leaves out -- genomic=True, longest
     protein, from_exons=True (exon features read as CDS) -- on random cases
-    with exon children (tests/test_fuzz.py)."""
-    rnd = random.Random(20261017)
+    with exon children (tests/test_fuzz.py).  fuzz4.json: 120 more from seed
+    20261020."""
+    rnd = random.Random(seed)
     out = []
     for i in range(n):
         fasta, gff = _fuzz_case2(rnd)
@@ -770,6 +772,8 @@ def main():
     if '--only-fuzz3' in sys.argv:
         with open(os.path.join(HERE, 'fuzz3.json'), 'w') as fh:
             json.dump(make_fuzz(ref, n=200, seed=20261017), fh, indent=0, sort_keys=True)
+        with open(os.path.join(HERE, 'fuzz4.json'), 'w') as fh:
+            json.dump(make_fuzz2(ref, n=120, seed=20261020), fh, indent=0, sort_keys=True)
         return
     if '--only-flank-edges' in sys.argv:
         with open(os.path.join(HERE, 'flank_edges.json'), 'w') as fh:
@@ -781,6 +785,8 @@ def main():
         json.dump(make_fuzz2(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'fuzz3.json'), 'w') as fh:
         json.dump(make_fuzz(ref, n=200, seed=20261017), fh, indent=0, sort_keys=True)
+    with open(os.path.join(HERE, 'fuzz4.json'), 'w') as fh:
+        json.dump(make_fuzz2(ref, n=120, seed=20261020), fh, indent=0, sort_keys=True)
     import genome_tools as ref_tools  # the reference's, from the same Python 3 copy
     with open(os.path.join(HERE, 'cds2pep.json'), 'w') as fh:
         json.dump(make_cds2pep(ref_tools), fh, indent=0, sort_keys=True)

@@ -26,7 +26,9 @@ from oracle import magot_oracle as mo
 CASES = json.load(open(os.path.join(goldlib.HERE, 'fuzz.json'))) + \
     json.load(open(os.path.join(goldlib.HERE, 'fuzz3.json')))
 # genomic=True, longest protein and from_exons=True (exon features as CDS)
-CASES2 = json.load(open(os.path.join(goldlib.HERE, 'fuzz2.json')))
+# (fuzz4.json: 120 more of them, another seed)
+CASES2 = json.load(open(os.path.join(goldlib.HERE, 'fuzz2.json'))) + \
+    json.load(open(os.path.join(goldlib.HERE, 'fuzz4.json')))
 
 
 def _sha(s):
