@@ -17,13 +17,15 @@ Outputs (data only: inputs, expected outputs, hashes):
   loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
   flank_edges.json extract_upstream_downstream on the native flank planner's edge cases
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
+  blast_fuzz.json blast_csv2fasta on random BLAST tables
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
   fuzz3.json      200 more of them (another seed)
   fuzz4.json      120 more cases of fuzz2.json's generator (another seed)
   translate_lib.json Sequence.translate with non-standard libraries, frames -6..6
 
 Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges |
-                                           --only-fuzz3 | --only-cds2pep2]
+                                           --only-fuzz3 | --only-cds2pep2 |
+                                           --only-blast-fuzz]
 """
 
 import contextlib
@@ -563,6 +565,59 @@ def make_matches(ref):
     return out
 
 
+def _blast_case(rnd):
+    """Random BLAST -outfmt 10 rows over _match_genome's contigs: repeated
+    queries (renamed q-1, q-2 ..), subjects running backwards or of one base,
+    coordinates at and past the contig ends, a truncated subject name, short
+    rows, CRLF lines; rarely a missing subject or a bad integer (the
+    reference raises)."""
+    subjects = ['chrA', 'chrA', 'chrB desc text', 'chrC']
+    lens = {'chrA': 1500, 'chrB desc text': 800, 'chrC': 300}
+    rows = []
+    for _ in range(rnd.randrange(0, 9)):
+        r = rnd.random()
+        if r < 0.08:
+            rows.append('short,row,only')
+            continue
+        q = 'q%d' % rnd.randrange(4)
+        s = rnd.choice(subjects)
+        a = rnd.randrange(1, lens[s] + 40)
+        b = a + rnd.choice([0, rnd.randrange(1, 120), -rnd.randrange(1, 120)])
+        b = max(b, 1)
+        if r > 0.97:
+            s = 'chrZ'
+        st, en = str(a), str(b)
+        if 0.95 < r <= 0.97:
+            en = 'x' + en
+        rows.append('%s,%s,95.0,60,3,0,1,60,%s,%s,1e-20,100' % (q, s, st, en))
+    eol = '\r\n' if rnd.random() < 0.2 else '\n'
+    return eol.join(rows) + (eol if rows and rnd.random() < 0.8 else '')
+
+
+def make_blast_fuzz(ref, n=100):
+    """genome_tools.blast_csv2fasta (:265-271) of the reference on random
+    BLAST tables over _match_genome(): stdout and exception
+    (tests/test_matches.py)."""
+    sys.path.insert(0, PY3)
+    import genome_tools as rt
+    import tempfile
+    rnd = random.Random(20261021)
+    fa_text = _match_genome()
+    cases = []
+    with tempfile.TemporaryDirectory() as td:
+        fa = os.path.join(td, 'g.fa')
+        with open(fa, 'w') as fh:
+            fh.write(fa_text)
+        for i in range(n):
+            csv = _blast_case(rnd)
+            path = os.path.join(td, 'b%d.csv' % i)
+            with open(path, 'w', newline='') as fh:
+                fh.write(csv)
+            _, exc, so = call(lambda: rt.blast_csv2fasta(fa, path))
+            cases.append({'csv': csv, 'exc': exc, 'stdout': so})
+    return {'genome': fa_text, 'cases': cases}
+
+
 def _fuzz_case(rnd):
     """A small random genome + GFF3 or GTF that walks many of read_gff's and
     get_fasta's branches: renamed duplicate IDs, reversed / zero / past-end
@@ -763,6 +818,10 @@ def main():
         json.dump(make_translate_lib(ref), fh, indent=0, sort_keys=True)
     if '--only-translate-lib' in sys.argv:
         return
+    if '--only-blast-fuzz' in sys.argv:
+        with open(os.path.join(HERE, 'blast_fuzz.json'), 'w') as fh:
+            json.dump(make_blast_fuzz(ref), fh, indent=0, sort_keys=True)
+        return
     if '--only-cds2pep2' in sys.argv:
         sys.path.insert(0, PY3)
         import genome_tools as ref_tools
@@ -794,6 +853,8 @@ def main():
         json.dump(make_cds2pep(ref_tools, n=160, seed=20261019), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'matches.json'), 'w') as fh:
         json.dump(make_matches(ref), fh, indent=1, sort_keys=True)
+    with open(os.path.join(HERE, 'blast_fuzz.json'), 'w') as fh:
+        json.dump(make_blast_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'loci.json'), 'w') as fh:
         json.dump(make_locus(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'flank_edges.json'), 'w') as fh:

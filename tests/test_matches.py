@@ -232,3 +232,38 @@ def test_get_seq_from_fasta_tool(files, key):
     text, exc, _ = _capture(genome_tools.get_seq_from_fasta, files['fa'], name, trunc)
     assert exc == GOLD[key]['exc']
     assert text == GOLD[key]['stdout']
+
+
+# ---------------------------------------------------------------------------
+# Random BLAST tables (tests/golden/blast_fuzz.json: the reference's stdout /
+# exception, make_golden.py --only-blast-fuzz)
+# ---------------------------------------------------------------------------
+
+BLAST_FUZZ = json.load(open(os.path.join(goldlib.HERE, 'blast_fuzz.json')))
+
+
+def _blast_files(tmp_path, k):
+    fa, csv = tmp_path / 'g.fa', tmp_path / 'b.csv'
+    fa.write_text(BLAST_FUZZ['genome'])
+    csv.write_bytes(BLAST_FUZZ['cases'][k]['csv'].encode('latin-1'))
+    return str(fa), str(csv)
+
+
+@pytest.mark.parametrize('k', range(len(BLAST_FUZZ['cases'])))
+def test_oracle_blast_fuzz_matches_reference(tmp_path, k):
+    fa, csv = _blast_files(tmp_path, k)
+    want = BLAST_FUZZ['cases'][k]
+    prints, exc, text = _capture(mo.blast_csv2fasta, fa, csv)
+    assert exc == want['exc']
+    assert (prints + text if exc is None else prints) == want['stdout']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('k', range(len(BLAST_FUZZ['cases'])))
+def test_gpu_blast_fuzz_matches_reference(tmp_path, k):
+    from magot_amd import genome_tools
+    fa, csv = _blast_files(tmp_path, k)
+    want = BLAST_FUZZ['cases'][k]
+    text, exc, _ = _capture(genome_tools.blast_csv2fasta, fa, csv, 'insertion')
+    assert exc == want['exc']
+    assert text == want['stdout']
