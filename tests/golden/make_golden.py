@@ -16,6 +16,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   synth_small.json hashes of gff2fasta on the seeded small synthetic
   loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
   flank_edges.json extract_upstream_downstream on the native flank planner's edge cases
+  flank_fuzz.json  extract_upstream_downstream on random GFFs
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
   blast_fuzz.json blast_csv2fasta on random BLAST tables
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
@@ -365,6 +366,57 @@ def make_flank_edges(ref):
             _, exc, so = call(lambda: rt.extract_upstream_downstream(fa_path, gff_path, n, stream,
                                                                     ft, nf, 'True'))
             cases.append({'gff': gff, 'sequence_length': n, 'stream': stream,
+                          'feature_type': ft, 'namefrom': nf, 'stdout': so, 'exc': exc})
+    return {'genome': FLANK_GENOME, 'cases': cases}
+
+
+def _flank_case(rnd):
+    """A random GFF and call for extract_upstream_downstream: the feature type
+    or others, every strand form, coordinates at and past the contig ends (0,
+    negative, swapped), names present, repeated, absent or holding '=', CRLF
+    and comment lines, lines with six tabs; lengths from 0 up and negative."""
+    rows = []
+    for _ in range(rnd.randint(0, 14)):
+        if rnd.random() < 0.08:
+            rows.append('#c1\tt\tgene\t1\t5\t.\t+\t.\tID=x')
+            continue
+        seqid = 'c1 first contig' if rnd.random() < 0.03 else rnd.choice(['c1', 'c2'])
+        ftype = rnd.choice(['gene', 'gene', 'gene', 'mRNA', 'CDS'])
+        a, b = rnd.randint(-5, 140), rnd.randint(-5, 140)
+        strand = rnd.choice(['.', '?']) if rnd.random() < 0.1 else rnd.choice(['+', '-'])
+        attrs = rnd.choice(['ID=g%d' % rnd.randint(0, 9),
+                            'ID=g%d;Name=n%d' % (rnd.randint(0, 9), rnd.randint(0, 9)),
+                            'Name=q', 'ID=a=b', 'x=1;ID=z;ID=w', ''])
+        cols = [seqid, 't', ftype, str(a), str(b), '.', strand]
+        if rnd.random() >= 0.1:
+            cols += ['.', attrs]
+        rows.append('\t'.join(cols))
+    gff = ''.join(r + ('\r\n' if rnd.random() < 0.2 else '\n') for r in rows)
+    n = rnd.choice(['0', '1', '4', '9', '30', '-2'])
+    stream = 'both' if rnd.random() < 0.05 else rnd.choice(['up', 'down'])
+    return gff, n, stream, rnd.choice(['gene', 'gene', 'mRNA']), rnd.choice(['ID', 'Name', 'x', ''])
+
+
+def make_flank_fuzz(ref, n=150):
+    """The reference's extract_upstream_downstream on random GFFs
+    (_flank_case) over FLANK_GENOME: stdout and exception (tests/test_flank.py)."""
+    sys.path.insert(0, PY3)
+    import genome_tools as rt
+    import tempfile
+    rnd = random.Random(20261022)
+    cases = []
+    with tempfile.TemporaryDirectory() as td:
+        fa_path = os.path.join(td, 'g.fa')
+        with open(fa_path, 'w') as fh:
+            fh.write(FLANK_GENOME)
+        for k in range(n):
+            gff, sl, stream, ft, nf = _flank_case(rnd)
+            gff_path = os.path.join(td, 'a%d.gff' % k)
+            with open(gff_path, 'w', newline='') as fh:
+                fh.write(gff)
+            _, exc, so = call(lambda: rt.extract_upstream_downstream(fa_path, gff_path, sl, stream,
+                                                                    ft, nf, 'True'))
+            cases.append({'gff': gff, 'sequence_length': sl, 'stream': stream,
                           'feature_type': ft, 'namefrom': nf, 'stdout': so, 'exc': exc})
     return {'genome': FLANK_GENOME, 'cases': cases}
 
@@ -837,6 +889,8 @@ def main():
     if '--only-flank-edges' in sys.argv:
         with open(os.path.join(HERE, 'flank_edges.json'), 'w') as fh:
             json.dump(make_flank_edges(ref), fh, indent=1, sort_keys=True)
+        with open(os.path.join(HERE, 'flank_fuzz.json'), 'w') as fh:
+            json.dump(make_flank_fuzz(ref), fh, indent=0, sort_keys=True)
         return
     with open(os.path.join(HERE, 'fuzz.json'), 'w') as fh:
         json.dump(make_fuzz(ref), fh, indent=0, sort_keys=True)
@@ -859,6 +913,8 @@ def main():
         json.dump(make_locus(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'flank_edges.json'), 'w') as fh:
         json.dump(make_flank_edges(ref), fh, indent=1, sort_keys=True)
+    with open(os.path.join(HERE, 'flank_fuzz.json'), 'w') as fh:
+        json.dump(make_flank_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'kat.json'), 'w') as fh:
         json.dump(make_kat(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'edge_cases.json'), 'w') as fh:

@@ -253,73 +253,45 @@ def test_gpu_flank_edges_match_reference(tmp_path, k):
         assert text == case['stdout']
 
 
-def _random_gff(rnd):
-    """A small GFF with the shapes extract_upstream_downstream meets: the
-    feature type or others, every strand form, coordinates at and past the
-    contig ends (0, negative, swapped), names present, repeated, absent or
-    holding '=', CRLF and comment lines, lines with six tabs."""
-    rows = []
-    for _ in range(rnd.randint(0, 14)):
-        kind = rnd.random()
-        if kind < 0.08:
-            rows.append('#' + 'c1\tt\tgene\t1\t5\t.\t+\t.\tID=x')
-            continue
-        seqid = 'c1 first contig' if rnd.random() < 0.03 else rnd.choice(['c1', 'c2'])
-        ftype = rnd.choice(['gene', 'gene', 'gene', 'mRNA', 'CDS'])
-        a, b = rnd.randint(-5, 140), rnd.randint(-5, 140)
-        strand = rnd.choice(['.', '?']) if rnd.random() < 0.1 else rnd.choice(['+', '-'])
-        attrs = rnd.choice(['ID=g%d' % rnd.randint(0, 9), 'ID=g%d;Name=n%d' % (rnd.randint(0, 9),
-                            rnd.randint(0, 9)), 'Name=q', 'ID=a=b', 'x=1;ID=z;ID=w', ''])
-        if rnd.random() < 0.1:
-            line = '\t'.join([seqid, 't', ftype, str(a), str(b), '.', strand])  # six tabs
-        else:
-            line = '\t'.join([seqid, 't', ftype, str(a), str(b), '.', strand, '.', attrs])
-        rows.append(line)
-    text = ''
-    for r in rows:
-        text += r + ('\r\n' if rnd.random() < 0.2 else '\n')
-    return text
+FUZZ = json.load(open(os.path.join(goldlib.HERE, 'flank_fuzz.json')))
 
 
-@pytest.mark.parametrize('seed', range(120))
-def test_native_flank_random_vs_oracle(tmp_path, seed):
-    """Random GFFs (seeded): the native planner renders the oracle's text, or
-    declines exactly where the oracle raises (the line loop then raises it)."""
-    import random
-    rnd = random.Random(seed)
-    fa, gf = tmp_path / 'g.fa', tmp_path / 'a.gff'
-    fa.write_text(FASTA)
-    gf.write_bytes(_random_gff(rnd).encode('latin-1'))
-    n = rnd.choice(['0', '1', '4', '9', '30', '-2'])
-    stream = 'both' if rnd.random() < 0.05 else rnd.choice(['up', 'down'])
-    nf = rnd.choice(['ID', 'Name', 'x', ''])
-    ft = rnd.choice(['gene', 'gene', 'mRNA'])
-    want, exc = _oracle(str(fa), str(gf), n, stream, ft, nf)
-    got = native_flank(str(fa), str(gf), n, stream, ft, nf)
+@pytest.mark.parametrize('k', range(len(FUZZ['cases'])))
+def test_flank_fuzz_matches_reference(tmp_path, k):
+    """tests/golden/flank_fuzz.json: the REFERENCE on 150 random GFFs (every
+    strand form, coordinates at and past the contig ends, names with '=', CRLF,
+    six-tab lines; make_golden.py _flank_case).  The oracle reproduces them;
+    the native planner renders the same text or declines where the
+    reference raises."""
+    case = FUZZ['cases'][k]
+    fa, gf, args = _fuzz_files(tmp_path, case)
+    want, exc = _oracle(fa, gf, *args)
+    assert exc == case['exc']
     if exc is None:
-        assert got == want
+        assert want == case['stdout']
+        assert native_flank(fa, gf, *args) == case['stdout']
     else:
-        assert got is None
+        assert native_flank(fa, gf, *args) is None
+
+
+def _fuzz_files(tmp_path, case):
+    fa, gf = tmp_path / 'g.fa', tmp_path / 'a.gff'
+    fa.write_text(FUZZ['genome'])
+    gf.write_bytes(case['gff'].encode('latin-1'))
+    return str(fa), str(gf), (case['sequence_length'], case['stream'], case['feature_type'],
+                              case['namefrom'])
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('seed', range(0, 120, 4))
-def test_gpu_flank_random_vs_oracle(tmp_path, seed):
-    """The random cases through the drop-in CLI function on the GPU."""
-    import random
-    rnd = random.Random(seed)
-    fa, gf = tmp_path / 'g.fa', tmp_path / 'a.gff'
-    fa.write_text(FASTA)
-    gf.write_bytes(_random_gff(rnd).encode('latin-1'))
-    n = rnd.choice(['0', '1', '4', '9', '30', '-2'])
-    stream = 'both' if rnd.random() < 0.05 else rnd.choice(['up', 'down'])
-    nf = rnd.choice(['ID', 'Name', 'x', ''])
-    ft = rnd.choice(['gene', 'gene', 'mRNA'])
-    want, exc = _oracle(str(fa), str(gf), n, stream, ft, nf)
+@pytest.mark.parametrize('k', range(len(FUZZ['cases'])))
+def test_gpu_flank_fuzz_matches_reference(tmp_path, k):
+    """The reference's random cases through the drop-in CLI function."""
+    case = FUZZ['cases'][k]
+    fa, gf, args = _fuzz_files(tmp_path, case)
     try:
-        got, gexc = _cli(str(fa), str(gf), n, stream, ft, nf), None
+        text, exc = _cli(fa, gf, *args), None
     except Exception as e:  # noqa: BLE001
-        got, gexc = None, type(e).__name__
-    assert gexc == exc
+        text, exc = None, type(e).__name__
+    assert exc == case['exc']
     if exc is None:
-        assert got == want
+        assert text == case['stdout']
