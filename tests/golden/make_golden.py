@@ -17,6 +17,7 @@ Outputs (data only: inputs, expected outputs, hashes):
   loci.json       extract_upstream_downstream / coords2fasta outputs (stdout)
   flank_edges.json extract_upstream_downstream on the native flank planner's edge cases
   flank_fuzz.json  extract_upstream_downstream on random GFFs
+  coords_fuzz.json coords2fasta on random windows of the O.biroi contigs
   matches.json    blast_csv2fasta / exonerate2fasta / get_seq_from_fasta outputs
   blast_fuzz.json blast_csv2fasta on random BLAST tables
   fuzz.json       random small GFF3/GTF cases through gff2fasta's path
@@ -26,7 +27,7 @@ Outputs (data only: inputs, expected outputs, hashes):
 
 Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges |
                                            --only-fuzz3 | --only-cds2pep2 |
-                                           --only-blast-fuzz]
+                                           --only-blast-fuzz | --only-coords-fuzz]
 """
 
 import contextlib
@@ -419,6 +420,31 @@ def make_flank_fuzz(ref, n=150):
             cases.append({'gff': gff, 'sequence_length': sl, 'stream': stream,
                           'feature_type': ft, 'namefrom': nf, 'stdout': so, 'exc': exc})
     return {'genome': FLANK_GENOME, 'cases': cases}
+
+
+def make_coords_fuzz(ref, n=60):
+    """The reference's coords2fasta (:656-661) on random windows of the
+    O.biroi contigs (starts at or below 0, stops past the end, reversed and
+    empty windows, a malformed number, a missing contig): stdout digest and
+    exception (tests/test_loci.py)."""
+    sys.path.insert(0, PY3)
+    import genome_tools as rt
+    rnd = random.Random(20261023)
+    fa = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
+    cases = []
+    for _ in range(n):
+        tr = rnd.choice(['True', 'False'])
+        seqs = mo.read_fasta(fa, truncate_names=tr == 'True')
+        name = rnd.choice(sorted(seqs) + ['absent'])
+        L = len(seqs.get(name, 'x' * 1000))
+        pick = lambda: str(rnd.choice([rnd.randint(-L - 10, L + 10), 0, 1, L, L + 1, -1]))
+        a, b = pick(), pick()
+        if rnd.random() < 0.05:
+            b = '12x'
+        _, exc, so = call(lambda: rt.coords2fasta(fa, name, a, b, tr))
+        cases.append({'seqid': name, 'start': a, 'stop': b, 'truncate_names': tr, 'exc': exc,
+                      'stdout_sha256': sha(so), 'stdout_head': so[:200]})
+    return cases
 
 
 def make_locus(ref):
@@ -870,6 +896,10 @@ def main():
         json.dump(make_translate_lib(ref), fh, indent=0, sort_keys=True)
     if '--only-translate-lib' in sys.argv:
         return
+    if '--only-coords-fuzz' in sys.argv:
+        with open(os.path.join(HERE, 'coords_fuzz.json'), 'w') as fh:
+            json.dump(make_coords_fuzz(ref), fh, indent=0, sort_keys=True)
+        return
     if '--only-blast-fuzz' in sys.argv:
         with open(os.path.join(HERE, 'blast_fuzz.json'), 'w') as fh:
             json.dump(make_blast_fuzz(ref), fh, indent=0, sort_keys=True)
@@ -915,6 +945,8 @@ def main():
         json.dump(make_flank_edges(ref), fh, indent=1, sort_keys=True)
     with open(os.path.join(HERE, 'flank_fuzz.json'), 'w') as fh:
         json.dump(make_flank_fuzz(ref), fh, indent=0, sort_keys=True)
+    with open(os.path.join(HERE, 'coords_fuzz.json'), 'w') as fh:
+        json.dump(make_coords_fuzz(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'kat.json'), 'w') as fh:
         json.dump(make_kat(ref), fh, indent=0, sort_keys=True)
     with open(os.path.join(HERE, 'edge_cases.json'), 'w') as fh:

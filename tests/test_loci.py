@@ -131,26 +131,29 @@ def test_gpu_coords2fasta_native_load(monkeypatch, tr):
     assert exc == 'KeyError' and text == '>no-such-contig:1-5\n'
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize('seed', range(40))
-def test_gpu_coords2fasta_random(seed):
-    """Seeded random windows on the O.biroi contigs (Python slice rules:
-    starts at or below 0, stops past the end, empty and reversed windows,
-    malformed numbers) through the native coords2fasta, against the oracle."""
-    import random
+COORDS_FUZZ = json.load(open(os.path.join(goldlib.HERE, 'coords_fuzz.json')))
 
-    from magot_amd import genome_tools
-    rnd = random.Random(seed)
+
+@pytest.mark.parametrize('k', range(len(COORDS_FUZZ)))
+def test_oracle_coords2fasta_fuzz_matches_reference(k):
+    """tests/golden/coords_fuzz.json: the REFERENCE's coords2fasta on random
+    windows of the O.biroi contigs (starts at or below 0, stops past the end,
+    reversed windows, a malformed number, a missing contig)."""
+    c = COORDS_FUZZ[k]
     fa = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
-    tr = rnd.choice(['True', 'False'])
-    seqs = mo.read_fasta(fa, truncate_names=tr == 'True')
-    name = rnd.choice(sorted(seqs) + ['absent'])
-    L = len(seqs.get(name, 'x' * 1000))
-    pick = lambda: str(rnd.choice([rnd.randint(-L - 10, L + 10), 0, 1, L, L + 1, -1]))
-    a, b = pick(), pick()
-    if rnd.random() < 0.05:
-        b = '12x'
-    want, exc = mo.coords2fasta(fa, name, a, b, tr)
-    text, gexc = _run_cli(genome_tools.coords2fasta, fa, name, a, b, tr)
-    assert gexc == (type(exc).__name__ if exc else None)
-    assert text == want
+    text, exc = mo.coords2fasta(fa, c['seqid'], c['start'], c['stop'], c['truncate_names'])
+    assert (type(exc).__name__ if exc else None) == c['exc']
+    assert _sha(text) == c['stdout_sha256']
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('k', range(len(COORDS_FUZZ)))
+def test_gpu_coords2fasta_fuzz_matches_reference(k):
+    """The same windows through the native coords2fasta."""
+    from magot_amd import genome_tools
+    c = COORDS_FUZZ[k]
+    fa = goldlib.path('O.biroi_refseqGenomeSubset.fasta')
+    text, exc = _run_cli(genome_tools.coords2fasta, fa, c['seqid'], c['start'], c['stop'],
+                         c['truncate_names'])
+    assert exc == c['exc']
+    assert _sha(text) == c['stdout_sha256']
