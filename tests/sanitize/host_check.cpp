@@ -3,7 +3,8 @@
 // Builds against the HOST translation units of libmagot (pack.cpp,
 // gffplan.cpp, fasta.cpp: the code that parses untrusted GFF / FASTA / CDS
 // text, with threads and hand-rolled hashing) compiled with
-// -fsanitize=address,undefined, and drives every host entry point over the
+// -fsanitize=address,undefined, and drives every host entry point (FASTA
+// reader and packer, gff2fasta and flank planners, cds2pep) over the
 // reference's fixture files, the generated parity cases and seeded mutations
 // of them.  Built and run by tests/sanitize/run.py; no GPU involved.
 //
@@ -204,6 +205,58 @@ static Genome do_fasta(const std::string& text, bool pack) {
 
 // --- GFF: magot_gff_plan under every flag combination, tables, render --------
 
+// tables, selections, render (sized, exact, one byte short) and the device
+// text units of one plan; destroys it
+static void check_plan(magot_gffplan* p, uint64_t ne, uint64_t nt) {
+  std::vector<magot_exon> ex(ne ? ne : 1);
+  std::vector<magot_tx> tx(nt ? nt : 1);
+  CHECK(magot_gffplan_tables(p, ex.data(), tx.data()) == 0, "tables");
+  uint64_t groups = 0;
+  CHECK(magot_gffplan_selections(p, &groups) == 0, "selections");
+  // payloads of the right sizes (nucleotide 'a'.., untrimmed peptide 'X'/'M')
+  std::vector<uint64_t> noff(nt + 1, 0), poff(nt + 1, 0);
+  for (uint64_t t = 0; t < nt; ++t) {
+    uint64_t len = 0;
+    CHECK(tx[t].exon_begin + tx[t].n_exons <= ne, "record %llu exons out of range",
+          (unsigned long long)t);
+    for (uint64_t e = tx[t].exon_begin; e < tx[t].exon_begin + tx[t].n_exons && e < ne; ++e)
+      len += ex[e].len;
+    noff[t + 1] = noff[t] + len;
+    poff[t + 1] = poff[t] + len / 3;
+  }
+  std::vector<uint8_t> nuc(noff[nt] + 1, 'a'), pep(poff[nt] + 1, 'M');
+  for (uint64_t t = 0; t < nt; ++t)
+    if (poff[t + 1] > poff[t] && (t & 1)) pep[poff[t]] = 'X';
+  uint64_t sz = 0;
+  int r2 = magot_gffplan_render(p, nuc.data(), noff.data(), pep.data(), poff.data(), nullptr, 0,
+                                &sz);
+  CHECK(r2 == 0, "render size: %s", g_err.c_str());
+  if (r2 == 0) {
+    std::vector<uint8_t> out(sz + 1);
+    r2 = magot_gffplan_render(p, nuc.data(), noff.data(), pep.data(), poff.data(), out.data(),
+                              sz, &sz);
+    CHECK(r2 == 0, "render: %s", g_err.c_str());
+    if (sz > 0) {
+      // one byte short: refused, not overrun
+      std::vector<uint8_t> small(sz - 1 ? sz - 1 : 1);
+      r2 = magot_gffplan_render(p, nuc.data(), noff.data(), pep.data(), poff.data(),
+                                small.data(), sz - 1, &sz);
+      CHECK(r2 != 0, "short render buffer accepted");
+    }
+  }
+  const std::string* text = nullptr;
+  std::vector<TextUnit> units;
+  bool protein = false;
+  uint64_t n_rec = 0;
+  if (gffplan_units(p, &text, &units, &protein, &n_rec)) {
+    for (const TextUnit& u : units) {
+      CHECK(u.text_off + u.text_len <= text->size(), "unit text range");
+      CHECK(u.rec == kNoRecord || u.rec < n_rec, "unit record");
+    }
+  }
+  magot_gffplan_destroy(p);
+}
+
 static int do_gff(const std::string& gff, const Genome& g, bool full) {
   std::vector<const char*> ids;
   for (auto& s : g.names) ids.push_back(s.c_str());
@@ -221,53 +274,40 @@ static int do_gff(const std::string& gff, const Genome& g, bool full) {
         continue;
       }
       ++planned;
-      std::vector<magot_exon> ex(ne ? ne : 1);
-      std::vector<magot_tx> tx(nt ? nt : 1);
-      CHECK(magot_gffplan_tables(p, ex.data(), tx.data()) == 0, "tables");
-      uint64_t groups = 0;
-      CHECK(magot_gffplan_selections(p, &groups) == 0, "selections");
-      // payloads of the right sizes (nucleotide 'a'.., untrimmed peptide 'X'/'M')
-      std::vector<uint64_t> noff(nt + 1, 0), poff(nt + 1, 0);
-      for (uint64_t t = 0; t < nt; ++t) {
-        uint64_t len = 0;
-        CHECK(tx[t].exon_begin + tx[t].n_exons <= ne, "record %llu exons out of range",
-              (unsigned long long)t);
-        for (uint64_t e = tx[t].exon_begin; e < tx[t].exon_begin + tx[t].n_exons && e < ne; ++e)
-          len += ex[e].len;
-        noff[t + 1] = noff[t] + len;
-        poff[t + 1] = poff[t] + len / 3;
-      }
-      std::vector<uint8_t> nuc(noff[nt] + 1, 'a'), pep(poff[nt] + 1, 'M');
-      for (uint64_t t = 0; t < nt; ++t)
-        if (poff[t + 1] > poff[t] && (t & 1)) pep[poff[t]] = 'X';
-      uint64_t sz = 0;
-      int r2 = magot_gffplan_render(p, nuc.data(), noff.data(), pep.data(), poff.data(), nullptr, 0,
-                                    &sz);
-      CHECK(r2 == 0, "render size: %s", g_err.c_str());
-      if (r2 == 0) {
-        std::vector<uint8_t> out(sz + 1);
-        r2 = magot_gffplan_render(p, nuc.data(), noff.data(), pep.data(), poff.data(), out.data(),
-                                  sz, &sz);
-        CHECK(r2 == 0, "render: %s", g_err.c_str());
-        if (sz > 0) {
-          // one byte short: refused, not overrun
-          std::vector<uint8_t> small(sz - 1 ? sz - 1 : 1);
-          r2 = magot_gffplan_render(p, nuc.data(), noff.data(), pep.data(), poff.data(),
-                                    small.data(), sz - 1, &sz);
-          CHECK(r2 != 0, "short render buffer accepted");
+      check_plan(p, ne, nt);
+    }
+  }
+  return planned;
+}
+
+// --- extract_upstream_downstream: magot_flank_plan ---------------------------
+
+static int do_flank(const std::string& gff, const Genome& g, bool full) {
+  std::vector<const char*> ids;
+  for (auto& s : g.names) ids.push_back(s.c_str());
+  int planned = 0;
+  static const char* kLengths[] = {"0", "1", "7", "100", " 3 ", "-2", "+5", "x", "99999999999"};
+  static const char* kNames[] = {"ID", "Name", "Parent", ""};
+  for (const char* len : kLengths) {
+    for (const char* stream : {"up", "down", "sideways"}) {
+      for (const char* ftype : {"gene", "CDS", "mRNA"}) {
+        for (const char* namefrom : kNames) {
+          if (!full && (ftype[0] != 'g' || namefrom[0] != 'I')) continue;
+          magot_gffplan* p = nullptr;
+          uint64_t ne = 0, nt = 0;
+          const int rc = magot_flank_plan(gff.data(), gff.size(), ids.data(), g.lens.data(),
+                                          (uint32_t)ids.size(), ftype, namefrom, len, stream, &p,
+                                          &ne, &nt);
+          if (rc) {
+            CHECK(p == nullptr, "flank plan handle on failure");
+            continue;
+          }
+          ++planned;
+          CHECK(ne == nt, "flank: one interval per record (%llu vs %llu)",
+                (unsigned long long)ne, (unsigned long long)nt);
+          check_plan(p, ne, nt);
         }
       }
-      const std::string* text = nullptr;
-      std::vector<TextUnit> units;
-      bool protein = false;
-      uint64_t n_rec = 0;
-      if (gffplan_units(p, &text, &units, &protein, &n_rec)) {
-        for (const TextUnit& u : units) {
-          CHECK(u.text_off + u.text_len <= text->size(), "unit text range");
-          CHECK(u.rec == kNoRecord || u.rec < n_rec, "unit record");
-        }
-      }
-      magot_gffplan_destroy(p);
     }
   }
   return planned;
@@ -352,7 +392,7 @@ int main(int argc, char** argv) {
   const int n_mut = argc > 2 ? atoi(argv[2]) : 20;
   std::ifstream list(argv[1]);
   std::string line;
-  int n_fa = 0, n_gff = 0, n_cds = 0, planned = 0, n_mutated = 0;
+  int n_fa = 0, n_gff = 0, n_cds = 0, planned = 0, flanks = 0, n_mutated = 0;
   Rng rng(20261017);
   while (std::getline(list, line)) {
     std::istringstream ls(line);
@@ -371,9 +411,15 @@ int main(int argc, char** argv) {
         setenv("MAGOT_GFF_CHUNKS", chunks, 1);
         planned += do_gff(t, g, chunks[0] == '1');
       }
+      for (const char* chunks : {"1", "5"}) {
+        setenv("MAGOT_GFF_CHUNKS", chunks, 1);
+        flanks += do_flank(t, g, chunks[0] == '1');
+      }
       setenv("MAGOT_GFF_CHUNKS", "3", 1);
       for (int k = 0; k < n_mut; ++k) {
-        do_gff(mutate(t, rng), g, false);
+        const std::string m = mutate(t, rng);
+        do_gff(m, g, false);
+        if (k < 8) do_flank(m, g, false);
         ++n_mutated;
       }
       unsetenv("MAGOT_GFF_CHUNKS");
@@ -386,7 +432,8 @@ int main(int argc, char** argv) {
     }
   }
   synthetic_packs();
-  printf("host_check: %d fasta, %d gff (%d plans, %d mutated gff), %d cds inputs; %d check "
-         "failure(s)\n", n_fa, n_gff, planned, n_mutated, n_cds, g_failures);
+  printf("host_check: %d fasta, %d gff (%d plans, %d flank plans, %d mutated gff), %d cds "
+         "inputs; %d check failure(s)\n", n_fa, n_gff, planned, flanks, n_mutated, n_cds,
+         g_failures);
   return g_failures ? 1 : 0;
 }
