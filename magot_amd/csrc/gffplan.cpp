@@ -40,7 +40,7 @@ struct Feature {
   int64_t lo = 0, hi = 0;
   uint32_t strand = 0;  // index into Model::strands
   bool base = false;
-  std::vector<uint32_t> children;  // child IDs (Model::ids)
+  uint32_t kids = ~0u;  // its child list (Model::kid_lists), ~0u: none yet
 };
 
 struct Table {
@@ -164,10 +164,23 @@ struct Model {
   std::unordered_map<std::string, uint32_t> table_index;
   std::vector<uint32_t> rank;      // table -> rank in sorted-name order
   std::vector<Feature> feats;
+  std::vector<std::vector<uint32_t>> kid_lists;  // child IDs (ids) per parent feature
 
   Model() {
     // AnnotationSet.__init__ (genome.py:528-533) creates these dicts
     for (const char* t : {"gene", "transcript", "CDS", "UTR"}) table(t);
+  }
+
+  const std::vector<uint32_t>& children(const Feature& f) const {
+    static const std::vector<uint32_t> none;
+    return f.kids == ~0u ? none : kid_lists[f.kids];
+  }
+  std::vector<uint32_t>& children_mut(Feature& f) {
+    if (f.kids == ~0u) {
+      f.kids = (uint32_t)kid_lists.size();
+      kid_lists.emplace_back();
+    }
+    return kid_lists[f.kids];
   }
 
   uint32_t id(sv s) { return id(s, hash_sv(s)); }
@@ -343,8 +356,8 @@ struct GffFormat {
 // the model: columns, coordinates, tags, the ID (before de-duplication) and
 // the parent / hierarchy values, each with its hash.
 struct GffLine {
-  sv id, parent, hv[2];
-  uint64_t h_id, h_parent, h_hv[2];
+  sv id, parent;
+  uint64_t h_id, h_parent;
   // j-th repeat of the previous line's ID (0: differs): the ordered pass
   // likely renames it to ID2 (j = 1) or ID-(j+1); h_dup is that name's hash
   uint64_t h_dup;
@@ -352,6 +365,13 @@ struct GffLine {
   int64_t lo, hi;
   uint32_t seqid, ftype, strand;  // chunk-local codes (LocalIntern)
   uint8_t has_parent, hv_mask;
+};
+
+// The hierarchy values of a GTF line (gene_id / transcript_id), kept beside
+// the lines only when the format has a hierarchy: GFF3's lines stay compact.
+struct GffHier {
+  sv hv[2];
+  uint64_t h_hv[2];
 };
 
 // Chunk-local string codes (seqid, type, strand) so that the ordered pass
@@ -455,7 +475,7 @@ struct LineParser {
   std::string dup;
 
   // false: the line is skipped; throws Unsupported on a diagnostic path
-  bool parse(const char* raw, uint64_t rl, GffLine& L) {
+  bool parse(const char* raw, uint64_t rl, GffLine& L, GffHier& H) {
     if (F.from_exons && sv(raw, rl).find("\texon\t") != sv::npos) {
       // line.replace("\texon\t", "\tCDS\t") (genome.py:285-286): left to right,
       // non-overlapping; the tab count (checked before, :283) is unchanged
@@ -542,8 +562,8 @@ struct LineParser {
       L.h_parent = hash_sv(L.parent);
       for (size_t level = 0; level < F.hierarchy.size(); ++level)
         if (const sv* pid = tags.get(F.hierarchy[level])) {
-          L.hv[level] = *pid;
-          L.h_hv[level] = hash_sv(*pid);
+          H.hv[level] = *pid;
+          H.h_hv[level] = hash_sv(*pid);
           L.hv_mask |= (uint8_t)(1u << level);
         }
     }
@@ -588,6 +608,8 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
     cut[c] = !nl ? n : (p ? (uint64_t)(nl - text) + 1 : 0);
   }
   std::vector<std::vector<GffLine>> lines(n_chunks);
+  std::vector<std::vector<GffHier>> hiers(n_chunks);  // GTF only
+  const bool hier = !F.hierarchy.empty();
   std::vector<std::unique_ptr<LineParser>> parsers(n_chunks);
   FirstError failed;
   std::atomic<bool> unsupported{false};
@@ -597,14 +619,20 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
       parsers[c].reset(new LineParser{F, {}, {}, {}});
       LineParser& P = *parsers[c];
       std::vector<GffLine>& out = lines[c];
+      std::vector<GffHier>& hout = hiers[c];
       out.reserve((cut[c + 1] - cut[c]) / 96 + 16);
+      if (hier) hout.reserve(out.capacity());
       try {
         GffLine L;
+        GffHier H;
         for (uint64_t pos = cut[c]; pos < cut[c + 1];) {
           const char* nl =
               static_cast<const char*>(memchr(text + pos, '\n', cut[c + 1] - pos));
           const uint64_t end = nl ? (uint64_t)(nl - text) + 1 : cut[c + 1];
-          if (P.parse(text + pos, end - pos, L)) out.push_back(L);
+          if (P.parse(text + pos, end - pos, L, H)) {
+            out.push_back(L);
+            if (hier) hout.push_back(H);
+          }
           pos = end;
         }
       } catch (const Unsupported&) {
@@ -648,6 +676,7 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
   int64_t last_k0 = -1, last_pk = -1;
   for (uint64_t c = 0; c < n_chunks; ++c) {
     const std::vector<GffLine>& V = lines[c];
+    const std::vector<GffHier>& HV = hiers[c];
     const LineParser& P = *parsers[c];
     sq_of.assign(P.seqids.strs.size(), ~0u);
     st_of.assign(P.strands.strs.size(), ~0u);
@@ -694,10 +723,10 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
         for (size_t level = 0; level < F.hierarchy.size(); ++level) {
           if (!((L.hv_mask >> level) & 1)) continue;
           const uint32_t t = hier_table[level];
-          const uint32_t pk = M.id(L.hv[level], L.h_hv[level]);
+          const uint32_t pk = M.id(HV[li].hv[level], HV[li].h_hv[level]);
           const int64_t have = M.slot(t, pk);
           if (have >= 0) {
-            auto& ch = M.feats[(size_t)have].children;
+            auto& ch = M.children_mut(M.feats[(size_t)have]);
             if (std::find(ch.begin(), ch.end(), child) == ch.end()) ch.push_back(child);
           } else {
             Feature f;
@@ -705,7 +734,7 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
             f.seqid = sq;
             f.strand = st;
             f.base = false;
-            f.children.push_back(child);
+            M.children_mut(f).push_back(child);
             M.feats.push_back(std::move(f));
             M.put(t, pk, (uint32_t)M.feats.size() - 1);
           }
@@ -721,10 +750,10 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
         Feature& holder = M.feats[(size_t)h];
         if (holder.base) throw Unsupported();  // BaseAnnotation has no child_list
         // without a hierarchy, a name interned on this line is in no child list yet
+        std::vector<uint32_t>& kids = M.children_mut(holder);
         if ((idk >= n_ids && F.hierarchy.empty()) ||
-            std::find(holder.children.begin(), holder.children.end(), idk) ==
-                holder.children.end())
-          holder.children.push_back(idk);
+            std::find(kids.begin(), kids.end(), idk) == kids.end())
+          kids.push_back(idk);
       }
       if (ty_of[L.ftype] == ~0u) {  // the table is created at the type's first line
         const sv ft = P.ftypes.strs[L.ftype];
@@ -873,15 +902,15 @@ struct Lowering {
   // Returns the number of records emitted ("" <=> 0).
   uint64_t fasta(uint32_t fi, bool first_in_join) {
     const Feature& F = M.feats[fi];
-    if (F.children.empty()) return 0;
-    const int64_t first = M.lookup(F.children[0]);
+    if (M.children(F).empty()) return 0;
+    const int64_t first = M.lookup(M.children(F)[0]);
     if (first < 0) throw Unsupported();  // KeyError
     if (M.feats[(size_t)first].base) {
       // base branch: child_dict keyed by coords (last wins), order by the last
       // child's strand, each child reverse-complemented by its own strand
       std::vector<std::pair<std::pair<int64_t, int64_t>, magot_exon>> by;
       uint32_t strand = 0;
-      for (uint32_t c : F.children) {
+      for (uint32_t c : M.children(F)) {
         const int64_t o = M.lookup(c);
         if (o < 0) throw Unsupported();
         const Feature& C = M.feats[(size_t)o];
@@ -927,7 +956,7 @@ struct Lowering {
     }
     if (longest) return fasta_longest(F);
     uint64_t n = 0;
-    for (uint32_t c : F.children) {
+    for (uint32_t c : M.children(F)) {
       const int64_t o = M.lookup(c);
       if (o < 0) throw Unsupported();
       if (M.feats[(size_t)o].base) throw Unsupported();  // mixed children: print
@@ -946,7 +975,7 @@ struct Lowering {
     Lowered best;
     uint64_t best_key = 0;
     bool have = false;
-    for (uint32_t c : F.children) {
+    for (uint32_t c : M.children(F)) {
       const int64_t o = M.lookup(c);
       if (o < 0) throw Unsupported();
       if (M.feats[(size_t)o].base) throw Unsupported();  // mixed children: print
@@ -969,7 +998,7 @@ struct Lowering {
   // so every candidate is lowered and the render picks (magot_gffplan_render).
   uint64_t fasta_longest_protein(const Feature& F) {
     std::vector<Lowered> cands;
-    for (uint32_t c : F.children) {
+    for (uint32_t c : M.children(F)) {
       const int64_t o = M.lookup(c);
       if (o < 0) throw Unsupported();
       if (M.feats[(size_t)o].base) throw Unsupported();  // mixed children: print
@@ -1019,8 +1048,8 @@ struct Lowering {
   // recursively.  A parent without children returns None, and the caller's
   // [0] raises TypeError.
   void coords(const Feature& F, int64_t& lo, int64_t& hi) const {
-    if (F.children.empty()) throw Unsupported();
-    for (uint32_t c : F.children) {
+    if (M.children(F).empty()) throw Unsupported();
+    for (uint32_t c : M.children(F)) {
       const int64_t o = M.lookup(c);
       if (o < 0) throw Unsupported();  // KeyError
       const Feature& C = M.feats[(size_t)o];
