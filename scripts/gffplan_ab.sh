@@ -2,7 +2,7 @@
 # A/B of the host gff2fasta planner on the C3 GFF3 (no GPU): two binaries
 # built from two versions of gffplan.cpp, run alternately on the same file.
 #   build here:  scripts/gffplan_ab.sh build OLD_GFFPLAN_CPP
-#   run:         scripts/gffplan_ab.sh run OUT_DIR [ROUNDS]
+#   run:         scripts/gffplan_ab.sh run OUT_DIR [ROUNDS]   (AB_TIMING=1: phase times)
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 F="-std=c++17 -O3 --offload-arch=gfx950 -x hip --offload-host-only -I$ROOT/include"
@@ -31,7 +31,8 @@ with open(os.path.join(d, 'ctgs.txt'), 'w') as fh:
 PY
 for i in $(seq "$ROUNDS"); do
   for v in old new; do
-    "$ROOT/scripts/gffplan_$v.bin" "$D/ann.gff3" "$D/ctgs.txt" 3 | sed "s/^/$v /" | tee -a "$OUT/gffplan_ab.txt"
+    env ${AB_TIMING:+MAGOT_GFF_TIMING=1} "$ROOT/scripts/gffplan_$v.bin" "$D/ann.gff3" "$D/ctgs.txt" 3 2>&1 |
+      sed "s/^/$v /" | tee -a "$OUT/gffplan_ab.txt"
   done
 done
 rm -rf "$D"
