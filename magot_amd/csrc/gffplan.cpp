@@ -82,15 +82,36 @@ inline uint64_t hash_sv(sv s) {
   return h ^ (h >> 29);
 }
 
+// Zero-filled words from calloc: a large table comes straight from the
+// kernel's zero pages instead of being written once by a fill and again by use.
+struct ZeroWords {
+  uint64_t* p = nullptr;
+  size_t n = 0;
+  explicit ZeroWords(size_t count) : p(static_cast<uint64_t*>(calloc(count, 8))), n(count) {
+    if (!p) throw std::bad_alloc();
+  }
+  ZeroWords(const ZeroWords&) = delete;
+  ZeroWords& operator=(const ZeroWords&) = delete;
+  ~ZeroWords() { free(p); }
+  size_t size() const { return n; }
+  uint64_t& operator[](size_t i) { return p[i]; }
+  const uint64_t& operator[](size_t i) const { return p[i]; }
+  void swap(ZeroWords& o) {
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+  }
+};
+
 struct Pool {
   std::vector<std::unique_ptr<char[]>> chunks;
   size_t left = 0;
   char* cur = nullptr;
   std::vector<sv> strs;
   // slot word: (hash bits for quick rejects) << 32 | (id + 1); 0 = empty
-  std::vector<uint64_t> slots{std::vector<uint64_t>(64, 0)};
+  ZeroWords slots{64};
 
   void reserve(size_t n) {
+    strs.reserve(n);
     size_t cap = 64;
     while (cap < 2 * n) cap <<= 1;
     if (cap > slots.size()) rehash(cap);
@@ -110,7 +131,7 @@ struct Pool {
   }
   static uint64_t word(uint64_t h, uint32_t id) { return (h >> 32 << 32) | (id + 1ull); }
   void rehash(size_t cap) {
-    std::vector<uint64_t> ns(cap, 0);
+    ZeroWords ns(cap);
     const size_t mask = cap - 1;
     for (uint32_t id = 0; id < strs.size(); ++id) {
       const uint64_t h = hash_sv(strs[id]);
@@ -665,6 +686,7 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
 
   // model updates in file order
   std::vector<uint32_t> renamed;  // per ID: 0, or the last suffix used
+  renamed.reserve(total + 16);
   std::string nid;
   std::vector<uint32_t> hier_table;
   for (const std::string& hk : F.hierarchy)
