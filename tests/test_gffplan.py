@@ -360,3 +360,31 @@ def test_native_from_exons_replace_and_substring_ignore():
                 assert got == want, (kw, seq_type)
                 planned += 1
     assert planned >= 2  # genomic and longest hit the reference's TypeError / ValueError on g2
+
+
+@pytest.mark.parametrize('fmt', ['gff3', 'gtf'])
+def test_native_plan_many_contigs(fmt):
+    """150 contigs, each with one gene: the planner's seqid table grows past its
+    initial 64 slots (rehash), and for GTF the hierarchy IDs outnumber the
+    lines the ID table was reserved for."""
+    import random
+    rng = random.Random(7)
+    fasta, gff = [], []
+    for i in range(150):
+        seq = ''.join(rng.choice('ACGT') for _ in range(90))
+        fasta.append('>chr%d\n%s\n' % (i, seq))
+        s = '+-'[i % 2]
+        if fmt == 'gff3':
+            gff.append('chr%d\tx\tgene\t1\t60\t.\t%s\t.\tID=g%d\n' % (i, s, i))
+            gff.append('chr%d\tx\tmRNA\t1\t60\t.\t%s\t.\tID=m%d;Parent=g%d\n' % (i, s, i, i))
+            gff.append('chr%d\tx\tCDS\t4\t30\t.\t%s\t0\tID=c%d;Parent=m%d\n' % (i, s, i, i))
+            gff.append('chr%d\tx\tCDS\t34\t57\t.\t%s\t0\tID=c%d;Parent=m%d\n' % (i, s, i, i))
+        else:
+            for lo, hi in ((4, 30), (34, 57)):
+                gff.append('chr%d\tx\tCDS\t%d\t%d\t.\t%s\t0\tgene_id "g%d"; transcript_id "t%d";\n'
+                           % (i, lo, hi, s, i, i))
+    fasta, gff = ''.join(fasta), ''.join(gff)
+    for seq_type in ('nucleotide', 'protein'):
+        got = native_gff2fasta(fasta, gff, seq_type, 'py2')
+        assert got is not None
+        assert got == mo.gff2fasta(fasta, gff, seq_type=seq_type, order='py2')
