@@ -124,11 +124,15 @@ def spawn_ranks(n, argv, script=None):
     return rc
 
 
-def dist_setup():
+def dist_setup(force=False):
+    """The process group of this rank (None for a single rank unless
+    ``force``: ``--dist`` runs the multi-rank job's collective path -- the
+    genome broadcast, the output gather, the reductions -- through a process
+    group of one rank, RCCL with the nccl backend)."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world == 1:
+    if world == 1 and not force:
         return None, rank, local, world
     import torch
     import torch.distributed as dist
@@ -172,6 +176,21 @@ def allreduce_max(dist, x):
 
 def allreduce_sum(dist, x):
     return _reduce(dist, x, None if dist is None else dist.ReduceOp.SUM)
+
+
+def all_values(dist, x):
+    """[x of rank 0, x of rank 1, ...] (float64 all_gather on the collective
+    device); [x] without a process group."""
+    if dist is None:
+        return [float(x)]
+    import torch
+
+    from magot_amd.shard import collective_device
+    dev = collective_device(dist)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    out = [torch.zeros(1, dtype=torch.float64, device=dev) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
 
 
 def settle(fn, sync, ms):
@@ -320,10 +339,16 @@ def cpu_baseline(w, budget_bases, orfs=False):
     cal_path = os.path.join(ROOT, 'profiles', 'cpu_calibration.json')
     if os.path.exists(cal_path) and not orfs and protein:  # calibrated on nucleotide + protein
         with open(cal_path) as fh:
-            ratio = json.load(fh)['port_over_reference_mean']
+            cj = json.load(fh)
+        ratio = cj['port_over_reference_mean']
+        lo, hi = cj.get('port_over_reference_min', ratio), cj.get('port_over_reference_max', ratio)
         # the reference's own loop (AnnotationSet.__getitem__ evals, genome.py:536-544)
-        # runs this much slower than the port on the same input (scripts/calibrate_cpu.py)
+        # runs this much slower than the port on the same input (scripts/calibrate_cpu.py,
+        # the C1 O.biroi subset, the rebuilt C14 and two synthetics)
         cal = {'reference_equivalent_bases_per_s': rate / ratio, 'port_over_reference': ratio,
+               'reference_equivalent_range': [rate / hi, rate / lo],
+               'port_over_reference_range': [lo, hi],
+               'rows': [r['workload'] for r in cj['rows']],
                'source': 'profiles/cpu_calibration.json'}
     return {'value': rate, 'unit': 'bases/s', 'cores': 1, 'kind': 'port', 'calibration': cal,
             'sample': '%d of %d transcripts (every %d-th), %d CDS bases; get_fasta nucleotide '
@@ -454,16 +479,24 @@ def run_job(args, dist, rank, local, world):
 
     from magot_amd import _lib, engine, shard, synth
     strong = args.mode == 'strong'
+    # one job over the process group (any world size, --dist at N=1): the
+    # genome is broadcast from rank 0 and the outputs gathered back to it
+    multi = strong and dist is not None
     c5 = args.config in ('C5', 'small5')
     t_start = t0 = time.perf_counter()
+    # the other ranks of a shared job make only the record tables (their
+    # stand-in for reading the GFF): the genome reaches them over the
+    # collective, and rank 0 checks the whole gathered job
     w = synth.make('small' if args.config == 'small5' else args.config,
-                   seed=shard_seed(args.config, 0 if strong else rank), order=args.order)
+                   seed=shard_seed(args.config, 0 if strong else rank), order=args.order,
+                   genome=not multi or rank == 0)
     t_gen = time.perf_counter() - t0
     log('generated %s: %d contigs, %d transcripts, %d exons, %d CDS bases (%.1fs)'
         % (args.config, len(w.contig_len), w.n_tx, w.n_exons, w.cds_bases, t_gen))
     ctx = _lib.Context(local)
 
-    mine, imb, t_bcast, t_pack, bcast_bytes = None, 0.0, None, None, None
+    mine, imb, t_bcast, t_pack, bcast_bytes, replica = None, 0.0, None, None, None, None
+    t_wait = 0.0  # waiting for rank 0's pack in the object broadcast
     shards = None
     rehearse = None
     if args.rehearse_shard and world == 1:
@@ -477,7 +510,7 @@ def run_job(args, dist, rank, local, world):
                                           tx_start=w.ex_start[first[:-1]])
         mine = sh[r]
         rehearse = {'ranks': k, 'rank': r, 'load_imbalance': shard.imbalance(load)}
-    if strong and world > 1:
+    if multi:
         first = np.zeros(w.n_tx + 1, dtype=np.int64)
         np.cumsum(w.ex_count, out=first[1:])
         tx_bases = np.add.reduceat(w.ex_len, first[:-1]) if w.n_tx else np.zeros(0)
@@ -487,9 +520,19 @@ def run_job(args, dist, rank, local, world):
         imb = shard.imbalance(load)
         log('%d records over %d ranks: load imbalance %.4f%%, %d contig(s) split'
             % (w.n_tx, world, 100.0 * imb, int((spans[:, 0] != spans[:, 1]).sum())))
-        dev, t_bcast, bcast_bytes = shard.replicate_genome(
-            dist, rank, w.contig_views() if rank == 0 else None, ctx)
-        t_bcast = allreduce_max(dist, t_bcast)
+        # at N=1 rank 0 extracts from the replica it rebuilds from its own
+        # wire image, so the receiving side runs too
+        dev, rep = shard.replicate_genome(
+            dist, rank, w.contig_views() if rank == 0 else None, ctx,
+            root_replica=world == 1)
+        t_wait = rep['meta_s']
+        t_bcast = allreduce_max(dist, rep['broadcast_s'])
+        bcast_bytes = rep['image_bytes'] + rep['meta_bytes']
+        replica = {'image_bytes': rep['image_bytes'], 'meta_bytes': rep['meta_bytes'],
+                   'export_s': rep['export_s'],
+                   'rebuild_s_max_rank': allreduce_max(dist, rep['rebuild_s']),
+                   'image': '2-bit forward codes + soft-mask runs + exception runs '
+                            '(magot_genome_wire_export); meta blob by object broadcast'}
     else:
         t0 = time.perf_counter()
         dev = engine.DeviceGenome(w.contig_views(), ctx=ctx)
@@ -523,7 +566,9 @@ def run_job(args, dist, rank, local, world):
     # -- correctness of the measured configuration (each rank, its own shard) -----
     parity = 'not checked'
     launches_before = 0  # launches of the measured kernel before the timed steps
-    if not args.no_verify:
+    if multi and not args.no_verify:
+        parity = 'checked on the gathered job (outputs_gather.parity)'
+    elif not args.no_verify:
         launches_before += 1
         t0 = time.perf_counter()
         ok = verify_orf6(w, plan, o6, mine) if c5 else verify_extract(w, plan, mine)
@@ -591,15 +636,25 @@ def run_job(args, dist, rank, local, world):
     phases['outputs_d2h_pinned'] = t_d2h
     del pin
     gather = None
-    if world > 1 and strong:
+    if multi:
         gather = gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx)
+        if rank == 0 and not args.no_verify:
+            parity = gather['parity']
     import resource
     rss_gb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2.0 ** 20  # KiB -> GiB
-    host = {'peak_rss_gib_max_rank': allreduce_max(dist, rss_gb),
+    rss_all = all_values(dist, rss_gb)
+    setup_all = all_values(dist, t_setup - t_wait)
+    wait_all = all_values(dist, t_wait)
+    host = {'peak_rss_gib_max_rank': max(rss_all),
             'peak_rss_gib_rank0': rss_gb,
-            'setup_s_max_rank': allreduce_max(dist, t_setup),
-            'setup': 'workload generation + genome pack or broadcast + plan upload, before '
-                     'the parity check'}
+            'peak_rss_gib_per_rank': rss_all,
+            'setup_s_max_rank': max(setup_all),
+            'setup_s_per_rank': setup_all,
+            'setup_wait_s_per_rank': wait_all,
+            'setup': 'own set-up work: workload generation (ranks > 0 of a shared job: record '
+                     'tables only) + genome pack, or the image broadcast and rebuild + plan '
+                     'upload, before the parity check; setup_wait_s: time the rank waited in '
+                     'the object broadcast for rank 0 to generate and pack the genome'}
 
     # -- roofline / traffic / baselines --------------------------------------------
     traffic = None
@@ -620,7 +675,10 @@ def run_job(args, dist, rank, local, world):
             cpu['c_port_all_cores'] = cpu_c_port(w, host_threads())
 
     if rank == 0:
-        if strong and world > 1:
+        if multi and world == 1:
+            label = '%s through the multi-GPU path at N=1 (%s process group of one rank)' \
+                % (args.config, dist.get_backend())
+        elif multi:
             label = 'C4: one %s job over %d GPUs' % (args.config, world) if args.config == 'C3' \
                 else '%s: one job over %d GPUs' % (args.config, world)
         elif strong:
@@ -680,9 +738,10 @@ def run_job(args, dist, rank, local, world):
             rec['rehearsal'] = rehearse
             rec['config']['workload'] = 'REHEARSAL (not a bench line): rank %d of a %d-rank ' \
                 '%s job on one GPU' % (rehearse['rank'], rehearse['ranks'], args.config)
-        if strong and world > 1:
+        if multi:
             rec['genome_broadcast_s'] = t_bcast
             rec['genome_broadcast_bytes'] = bcast_bytes
+            rec['genome_replica'] = replica
             rec['genome_arena_bytes'] = int(dev.device_bytes)
             rec['load_imbalance'] = imb
             rec['outputs_gather'] = gather
@@ -799,6 +858,10 @@ def main(argv=None):
     ap.add_argument('--mode', default='strong', choices=['strong', 'weak'],
                     help='strong (default): one job over N GPUs, genome broadcast, records '
                          'sharded (C3 at N=1, C4 at N>1); weak: one job per rank')
+    ap.add_argument('--dist', action='store_true',
+                    help='create the process group even for one rank (nccl = RCCL on a GPU): '
+                         'the N=1 job takes the multi-GPU path (genome broadcast from the '
+                         'wire image, output gather, reassembly, collective reductions)')
     ap.add_argument('--rehearse-shard', default=None, metavar='K:r',
                     help='diagnostic, one GPU: run only rank r\'s shard of a K-rank strong job '
                          '(the per-GPU work of the K-GPU line; not a bench line)')
@@ -806,15 +869,20 @@ def main(argv=None):
     args = ap.parse_args(raw)
     if args.rehearse_shard and args.gpus > 1:
         ap.error('--rehearse-shard runs one rank')
+    if args.rehearse_shard and args.dist:
+        ap.error('--rehearse-shard runs without a process group')
     if args.pmc_json is None:
         args.pmc_json = os.path.join(ROOT, 'profiles', 'pmc_%s.json' % args.config)
 
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
         return spawn_ranks(args.gpus, raw)
+    if args.dist and 'WORLD_SIZE' not in os.environ:
+        os.environ.update(WORLD_SIZE='1', RANK='0', LOCAL_RANK='0', MASTER_ADDR='127.0.0.1',
+                          MASTER_PORT=str(_free_port()))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world != args.gpus:
         log('--gpus %d but WORLD_SIZE=%d: running %d rank(s)' % (args.gpus, world, world))
-    dist, rank, local, world = dist_setup()
+    dist, rank, local, world = dist_setup(force=args.dist)
     if os.environ.get('MAGOT_DIST_BACKEND') == 'gloo':
         import torch
         local = local % max(torch.cuda.device_count(), 1)

@@ -195,6 +195,27 @@ int magot_genome_attach(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len, 
 int magot_genome_wire_ranges(const magot_genome* g, uint64_t* off, uint64_t* len, uint32_t* n);
 int magot_genome_attach_wire(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len,
                              void* arena_dev, magot_genome** out);
+/*
+ * The compact replica image (what a multi-GPU job broadcasts; the north
+ * star's 2-bit-packed genome): the forward strand's 2-bit codes (span/4
+ * bytes), the soft-masked bases as sorted {start, end} u32 runs plus a
+ * directory of one u32 per 4096 bases, and the arena's exception runs +
+ * directory verbatim -- every GenomeSequence byte (genome.py:854-877), about
+ * 0.27 B per base against the arena's 1 B.
+ *   magot_genome_wire_export  writes the image of g into caller device memory
+ *       of cap bytes (wire_dev == NULL: *wire_bytes only).  Synchronous.
+ *   magot_genome_wire_import  a genome in its own new arena (freed by
+ *       magot_genome_destroy) rebuilt on ctx's device from an image in device
+ *       memory and the genome's meta blob (magot_genome_export): the nibble
+ *       plane is unpacked and the mirror derived there; the arena equals the
+ *       packed original byte for byte.  The image may be freed on return.
+ *       An image that does not match the meta is refused (MAGOT_ERR_ARG).
+ * No reference counterpart (the reference is single-process).
+ */
+int magot_genome_wire_export(const magot_genome* g, void* wire_dev, uint64_t cap,
+                             uint64_t* wire_bytes);
+int magot_genome_wire_import(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len,
+                             const void* wire_dev, uint64_t wire_bytes, magot_genome** out);
 
 /*
  * Reassembly of a sharded job's outputs on one device (outputs
@@ -202,6 +223,7 @@ int magot_genome_attach_wire(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_
  * i < n, dst[dst_off[i], dst_off[i+1]) = src[src_off[i], src_off[i] +
  * dst_off[i+1] - dst_off[i]).  src (src_bytes long) and dst (dst_off[n] long)
  * are device memory (e.g. the buffer an RCCL gather filled, rank-major),
+ * both 16-byte aligned (else MAGOT_ERR_ARG),
  * dst_off has n+1 non-decreasing entries, the offset tables are host arrays;
  * a segment reaching past src_bytes is refused (MAGOT_ERR_RANGE) before any
  * launch.  Synchronous.  No reference counterpart (the reference is
@@ -342,6 +364,9 @@ int magot_codon_symbols(magot_ctx* ctx, const uint8_t* seq, uint64_t n_codons,
  */
 int magot_orf6_sizes(const uint64_t* seq_off, uint64_t n, uint64_t* stream_off,
                      uint64_t* stream_len, uint8_t* none_mask);
+/* magot_orf6_batch: stream_off must be exactly magot_orf6_sizes' table for
+ * seq_off (the kernel places every stream from its record's block start and
+ * length); any other table is refused with MAGOT_ERR_ARG before a launch. */
 int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_off, uint64_t n,
                      const uint8_t* lut64, const uint64_t* stream_off, uint8_t* out);
 /* The same over an extraction plan's records, in HBM (BASELINE configs[4],

@@ -43,6 +43,7 @@ EXPORTS = (
     'magot_fasta_text_time', 'magot_fasta_text_destroy',
     'magot_genome_load_ex', 'magot_genome_wire_ranges', 'magot_genome_attach_wire',
     'magot_copy_segments', 'magot_ctx_mark', 'magot_ctx_elapsed', 'magot_orf6_copy_outputs',
+    'magot_genome_wire_export', 'magot_genome_wire_import',
 )
 
 ERR_UNSUPPORTED = -5
@@ -153,6 +154,9 @@ def _declare(lib):
                                                     ctypes.POINTER(ctypes.c_uint32)]),
         'magot_genome_attach_wire': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp,
                                                     ctypes.POINTER(_vp)]),
+        'magot_genome_wire_export': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _u64p]),
+        'magot_genome_wire_import': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp,
+                                                    ctypes.c_uint64, ctypes.POINTER(_vp)]),
         'magot_copy_segments': (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, _vp, _vp,
                                                ctypes.c_uint64]),
         'magot_ctx_mark': (ctypes.c_int, [_vp, ctypes.c_int]),

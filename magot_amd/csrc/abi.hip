@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <thread>
 
 #include "common.h"
@@ -42,9 +43,11 @@ struct magot_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t mark0 = nullptr, mark1 = nullptr;  // magot_ctx_mark
-  // pinned staging ring for genome uploads (allocated on first use)
+  // pinned staging ring for genome uploads (allocated on first use); loads on
+  // one context from several host threads take turns on it
   uint8_t* pin[2] = {nullptr, nullptr};
   hipEvent_t pin_ev[2] = {nullptr, nullptr};
+  std::mutex pin_mu;
 };
 
 struct magot_genome {
@@ -156,6 +159,19 @@ std::vector<uint8_t> genome_meta(const magot_genome* g) {
   w.put_vec(g->host_runs);
   w.put_vec(g->host_dir);
   return w.buf;
+}
+
+// Parse a meta blob into g's host fields; the piece offsets into *o.
+bool parse_genome_meta(const uint8_t* meta, uint64_t meta_len, magot_genome* g, uint64_t o[3]) {
+  MetaReader r{meta, meta + meta_len};
+  uint64_t magic = 0;
+  bool ok = r.get(&magic) && magic == kMetaMagic && r.get(&g->arena_bytes) && r.get(&o[0]) &&
+            r.get(&o[1]) && r.get(&o[2]) && r.get(&g->span) && r.get(&g->extent) &&
+            r.get(&g->total_bases) && r.get(&g->n_runs) && r.get_vec(&g->contig_base) &&
+            r.get_vec(&g->contig_len) && r.get_vec(&g->host_runs) && r.get_vec(&g->host_dir);
+  return ok && o[0] < g->arena_bytes && o[1] < g->arena_bytes && o[2] < g->arena_bytes &&
+         g->host_runs.size() == g->n_runs + 1 && g->span % 32 == 0 &&
+         o[0] + (2 * (g->span / 8) + 4) * 4 <= o[1] && o[1] <= o[2];
 }
 
 // Pack the contigs and place the planes in HBM (magot_genome_load*): on the
@@ -319,6 +335,7 @@ int upload_raw(magot_ctx* ctx, const ContigSource* src, const HostPacked& lay, u
   const uint64_t total = lay.extent - kOrigin;
   if (!total) return MAGOT_OK;
   constexpr uint64_t kRing = 64ull << 20;
+  std::lock_guard<std::mutex> lock(ctx->pin_mu);
   for (int k = 0; k < 2; ++k)
     if (!ctx->pin[k]) {
       MAGOT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pin[k]), kRing, hipHostMallocDefault));
@@ -341,7 +358,9 @@ int upload_raw(magot_ctx* ctx, const ContigSource* src, const HostPacked& lay, u
   for (uint64_t q0 = 0, k = 0; q0 < total; q0 += kRing, ++k) {
     const int b = (int)(k & 1);
     const uint64_t q1 = std::min(total, q0 + kRing);
-    if (k >= 2) MAGOT_HIP_TRY(hipEventSynchronize(ctx->pin_ev[b]));
+    // the buffer's previous DMA (of this load, or of an earlier one whose
+    // last copies may still be in flight) has drained
+    MAGOT_HIP_TRY(hipEventSynchronize(ctx->pin_ev[b]));
     const uint64_t step = ((q1 - q0) + nt - 1) / nt;
     std::vector<std::thread> pool;
     for (unsigned i = 1; i < nt && q0 + i * step < q1; ++i) {
@@ -646,13 +665,8 @@ int magot_genome_attach(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len, 
   }
   *out = nullptr;
   std::unique_ptr<magot_genome> g(new magot_genome());
-  MetaReader r{meta, meta + meta_len};
-  uint64_t magic = 0, o_nib = 0, o_runs = 0, o_dir = 0;
-  bool ok = r.get(&magic) && magic == kMetaMagic && r.get(&g->arena_bytes) && r.get(&o_nib) &&
-            r.get(&o_runs) && r.get(&o_dir) && r.get(&g->span) && r.get(&g->extent) &&
-            r.get(&g->total_bases) && r.get(&g->n_runs) && r.get_vec(&g->contig_base) &&
-            r.get_vec(&g->contig_len) && r.get_vec(&g->host_runs) && r.get_vec(&g->host_dir);
-  if (!ok || o_nib >= g->arena_bytes || o_runs >= g->arena_bytes || o_dir >= g->arena_bytes) {
+  uint64_t o[3];
+  if (!parse_genome_meta(meta, meta_len, g.get(), o)) {
     set_error("magot_genome_attach: malformed genome meta");
     return MAGOT_ERR_ARG;
   }
@@ -660,9 +674,9 @@ int magot_genome_attach(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len, 
   g->arena = arena_dev;
   g->owns_arena = false;
   char* base = static_cast<char*>(arena_dev);
-  g->nib = reinterpret_cast<uint32_t*>(base + o_nib);
-  g->runs = reinterpret_cast<ExcRun*>(base + o_runs);
-  g->dir = reinterpret_cast<uint32_t*>(base + o_dir);
+  g->nib = reinterpret_cast<uint32_t*>(base + o[0]);
+  g->runs = reinterpret_cast<ExcRun*>(base + o[1]);
+  g->dir = reinterpret_cast<uint32_t*>(base + o[2]);
   *out = g.release();
   return MAGOT_OK;
 }
@@ -709,6 +723,151 @@ int magot_genome_attach_wire(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_
   return MAGOT_OK;
 }
 
+// --- the compact replica image (wire.hip) ---------------------------------
+
+namespace {
+
+uint64_t fnv1a(const uint8_t* p, uint64_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint64_t i = 0; i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+  return h;
+}
+
+// The image layout of a genome (span bases, arena_bytes with the exception
+// runs at runs_off, meta blob hash) with n_mask soft-mask runs.
+WireHeader wire_layout(uint64_t span, uint64_t arena_bytes, uint64_t runs_off, uint64_t n_mask,
+                       uint64_t meta_hash) {
+  WireHeader h{};
+  h.magic = kWireMagic;
+  h.meta_hash = meta_hash;
+  h.span = span;
+  h.n_mask = n_mask;
+  h.n_mdir = (span >> kDirShift) + 2;
+  Carve cv;
+  cv.take<WireHeader>(1);
+  h.o_code2 = cv.take<uint32_t>(span / 16);
+  h.o_mask = cv.take<uint32_t>(2 * (n_mask + 1));
+  h.o_mdir = cv.take<uint32_t>(h.n_mdir);
+  h.exc_bytes = arena_bytes - runs_off;
+  h.o_exc = cv.take<uint8_t>(h.exc_bytes);
+  h.total = cv.used;
+  return h;
+}
+
+}  // namespace
+
+int magot_genome_wire_export(const magot_genome* g, void* wire_dev, uint64_t cap,
+                             uint64_t* wire_bytes) {
+  if (!g || !wire_bytes) {
+    set_error("magot_genome_wire_export: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (int rc = bind(g->ctx)) return rc;
+  hipStream_t st = g->ctx->stream;
+  const uint64_t groups = g->span / 32;
+  const size_t scan_bytes = wire_scan_bytes(groups);
+  Carve sc;
+  const uint64_t o_cnt = sc.take<uint32_t>(groups + 1);
+  const uint64_t o_slot = sc.take<uint64_t>(groups + 1);
+  const uint64_t o_tmp = sc.take<uint8_t>(scan_bytes + 1);
+  DevBuf scratch;
+  MAGOT_HIP_TRY(hipMalloc(&scratch.p, sc.used));
+  char* sb = static_cast<char*>(scratch.p);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(sb + o_cnt);
+  uint64_t* slot = reinterpret_cast<uint64_t*>(sb + o_slot);
+  MAGOT_HIP_TRY(launch_wire_count(g->nib, g->span, cnt, slot, sb + o_tmp, scan_bytes, st));
+  uint64_t n_mask = 0;
+  if (groups) {
+    uint64_t last_slot = 0;
+    uint32_t last_cnt = 0;
+    MAGOT_HIP_TRY(hipMemcpyAsync(&last_slot, slot + groups - 1, 8, hipMemcpyDeviceToHost, st));
+    MAGOT_HIP_TRY(hipMemcpyAsync(&last_cnt, cnt + groups - 1, 4, hipMemcpyDeviceToHost, st));
+    MAGOT_HIP_TRY(hipStreamSynchronize(st));
+    n_mask = last_slot + last_cnt;
+  }
+  const std::vector<uint8_t> meta = genome_meta(g);
+  const WireHeader h = wire_layout(g->span, g->arena_bytes,
+                                   (uint64_t)((const char*)g->runs - (const char*)g->arena), n_mask,
+                                   fnv1a(meta.data(), meta.size()));
+  *wire_bytes = h.total;
+  if (!wire_dev) return MAGOT_OK;
+  if (cap < h.total) {
+    set_error("magot_genome_wire_export: image buffer too small");
+    return MAGOT_ERR_ARG;
+  }
+  char* wb = static_cast<char*>(wire_dev);
+  uint32_t* runs = reinterpret_cast<uint32_t*>(wb + h.o_mask);
+  launch_code2(g->nib, g->span / 8, reinterpret_cast<uint32_t*>(wb + h.o_code2), st);
+  MAGOT_HIP_TRY(hipGetLastError());
+  launch_wire_runs(g->nib, g->span, slot, runs, st);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipMemsetAsync(runs + 2 * n_mask, 0xFF, 8, st));  // sentinel {~0, ~0}
+  launch_wire_mdir(runs, n_mask, h.n_mdir, reinterpret_cast<uint32_t*>(wb + h.o_mdir), st);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipMemcpyAsync(wb + h.o_exc, g->runs, h.exc_bytes, hipMemcpyDeviceToDevice, st));
+  MAGOT_HIP_TRY(hipMemcpyAsync(wb, &h, sizeof(h), hipMemcpyHostToDevice, st));
+  MAGOT_HIP_TRY(hipStreamSynchronize(st));
+  return MAGOT_OK;
+}
+
+int magot_genome_wire_import(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_len,
+                             const void* wire_dev, uint64_t wire_bytes, magot_genome** out) {
+  if (int rc = bind(ctx)) return rc;
+  if (!meta || !wire_dev || !out) {
+    set_error("magot_genome_wire_import: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  std::unique_ptr<magot_genome> g(new magot_genome());
+  uint64_t o[3];
+  if (!parse_genome_meta(meta, meta_len, g.get(), o)) {
+    set_error("magot_genome_wire_import: malformed genome meta");
+    return MAGOT_ERR_ARG;
+  }
+  if (wire_bytes < sizeof(WireHeader)) {
+    set_error("magot_genome_wire_import: image too small");
+    return MAGOT_ERR_ARG;
+  }
+  WireHeader h{};
+  MAGOT_HIP_TRY(hipMemcpyAsync(&h, wire_dev, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  g->ctx = ctx;
+  // the image must have been cut from the genome the meta describes
+  const WireHeader want = wire_layout(g->span, g->arena_bytes, o[1], h.n_mask,
+                                      fnv1a(meta, meta_len));
+  if (h.magic != kWireMagic || h.total > wire_bytes || h.n_mask >= (1ull << 32) ||
+      std::memcmp(&h, &want, sizeof(h)) != 0) {
+    set_error("magot_genome_wire_import: image does not match the genome meta");
+    return MAGOT_ERR_ARG;
+  }
+  DevBuf arena;  // owned by the genome once everything below succeeded
+  MAGOT_HIP_TRY(hipMalloc(&arena.p, g->arena_bytes));
+  g->arena = arena.p;
+  g->owns_arena = true;
+  char* base = static_cast<char*>(g->arena);
+  g->nib = reinterpret_cast<uint32_t*>(base + o[0]);
+  g->runs = reinterpret_cast<ExcRun*>(base + o[1]);
+  g->dir = reinterpret_cast<uint32_t*>(base + o[2]);
+  const char* wb = static_cast<const char*>(wire_dev);
+  const ExcRun* w_exc = reinterpret_cast<const ExcRun*>(wb + h.o_exc);
+  const uint32_t* w_edir = reinterpret_cast<const uint32_t*>(wb + h.o_exc + (o[2] - o[1]));
+  const uint64_t nw = g->span / 8;
+  hipStream_t st = ctx->stream;
+  launch_wire_unpack(reinterpret_cast<const uint32_t*>(wb + h.o_code2),
+                     reinterpret_cast<const uint32_t*>(wb + h.o_mask), h.n_mask,
+                     reinterpret_cast<const uint32_t*>(wb + h.o_mdir), h.n_mdir, w_exc, g->n_runs,
+                     w_edir, g->host_dir.size(), g->span, g->nib, st);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipMemsetAsync(g->nib + 2 * nw, 0, 16, st));
+  launch_mirror_planes(g->nib, g->span, st);
+  MAGOT_HIP_TRY(hipGetLastError());
+  MAGOT_HIP_TRY(hipMemcpyAsync(g->runs, w_exc, h.exc_bytes, hipMemcpyDeviceToDevice, st));
+  MAGOT_HIP_TRY(hipStreamSynchronize(st));
+  arena.p = nullptr;
+  *out = g.release();
+  return MAGOT_OK;
+}
+
 int magot_copy_segments(magot_ctx* ctx, const void* src_dev, uint64_t src_bytes, void* dst_dev,
                         const uint64_t* src_off, const uint64_t* dst_off, uint64_t n) {
   if (int rc = bind(ctx)) return rc;
@@ -719,6 +878,13 @@ int magot_copy_segments(magot_ctx* ctx, const void* src_dev, uint64_t src_bytes,
   if (!n || dst_off[n] == dst_off[0]) return MAGOT_OK;
   if (!src_dev || !dst_dev) {
     set_error("magot_copy_segments: null buffer");
+    return MAGOT_ERR_ARG;
+  }
+  // the kernel reads whole 16-byte blocks of src (each holds a byte of its
+  // segment, so an aligned block never leaves the allocation's pages) and
+  // stores 16-byte chunks at 16-aligned dst offsets
+  if ((reinterpret_cast<uintptr_t>(src_dev) | reinterpret_cast<uintptr_t>(dst_dev)) & 15u) {
+    set_error("magot_copy_segments: src and dst must be 16-byte aligned");
     return MAGOT_ERR_ARG;
   }
   for (uint64_t i = 0; i < n; ++i) {
@@ -1392,6 +1558,22 @@ int magot_orf6_batch(magot_ctx* ctx, const uint8_t* seqs, const uint64_t* seq_of
   if (!seq_off || !stream_off) {
     set_error("magot_orf6_batch: null argument");
     return MAGOT_ERR_ARG;
+  }
+  for (uint64_t r = 0; r < n; ++r)
+    if (seq_off[r + 1] < seq_off[r]) {
+      set_error("magot_orf6_batch: seq_off must be non-decreasing");
+      return MAGOT_ERR_ARG;
+    }
+  {
+    // the kernel places each stream from its record's block start and length
+    // (magot_orf6_sizes' layout); a different table would send its stores
+    // past the caller's buffer, so it is refused
+    std::vector<uint64_t> want(6 * n + 1);
+    magot_orf6_sizes(seq_off, n, want.data(), nullptr, nullptr);
+    if (std::memcmp(want.data(), stream_off, want.size() * 8) != 0) {
+      set_error("magot_orf6_batch: stream_off is not magot_orf6_sizes' table for seq_off");
+      return MAGOT_ERR_ARG;
+    }
   }
   const uint64_t total = n ? seq_off[n] : 0, total_res = n ? stream_off[6 * n] : 0;
   if (total_res == 0) return MAGOT_OK;

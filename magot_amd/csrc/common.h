@@ -99,6 +99,34 @@ void launch_nib_pack(const uint8_t* raw, uint64_t n, uint32_t* nib, uint64_t nib
 void launch_segments_copy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off,
                           uint64_t n, uint8_t* dst, hipStream_t s);
 
+// Compact replica image of a packed genome (wire.hip; magot_genome_wire_*).
+constexpr uint64_t kWireMagic = 0x3257544f47414d00ull;  // "\0MAGOTW2"
+struct WireHeader {
+  uint64_t magic;
+  uint64_t span;       // of the genome it was cut from
+  uint64_t n_mask;     // soft-mask runs (the sentinel pair follows them)
+  uint64_t n_mdir;     // mask directory entries
+  uint64_t o_code2, o_mask, o_mdir, o_exc;  // byte offsets in the image
+  uint64_t exc_bytes;  // the arena's exception runs + directory region
+  uint64_t total;      // image bytes
+  uint64_t meta_hash;  // FNV-1a of the genome's meta blob (magot_genome_export)
+};
+size_t wire_scan_bytes(uint64_t groups);
+// count[g] = soft-mask runs starting in bases [32g, 32g+32) of the forward
+// plane; slot = their exclusive prefix sum (span / 32 entries each)
+hipError_t launch_wire_count(const uint32_t* nib, uint64_t span, uint32_t* count, uint64_t* slot,
+                             void* scan_tmp, size_t scan_bytes, hipStream_t s);
+// every mask run's {start, end} at its slot (u32 pairs)
+void launch_wire_runs(const uint32_t* nib, uint64_t span, const uint64_t* slot, uint32_t* runs,
+                      hipStream_t s);
+void launch_wire_mdir(const uint32_t* runs, uint64_t n, uint64_t n_blocks, uint32_t* mdir,
+                      hipStream_t s);
+// the forward nibble plane (span / 8 words) from an image's pieces
+void launch_wire_unpack(const uint32_t* code2, const uint32_t* mask, uint64_t n_mask,
+                        const uint32_t* mdir, uint64_t n_mdir, const ExcRun* exc, uint64_t n_exc,
+                        const uint32_t* edir, uint64_t n_edir, uint64_t span, uint32_t* nib,
+                        hipStream_t s);
+
 // ---------------------------------------------------------------------------
 // Extraction tiling
 // ---------------------------------------------------------------------------
@@ -118,17 +146,11 @@ constexpr int tile_bytes(int lane_chunks) { return (64 * lane_chunks - 3) * 16; 
 // plans whose large-tile count is below this use the small tile
 constexpr uint64_t kSmallTilePlan = 40000;
 // extraction tiles end on this output boundary where they can (bytes)
-#ifndef MAGOT_EXP_TILE_ALIGN
-#define MAGOT_EXP_TILE_ALIGN 128
-#endif
-constexpr uint64_t kTileAlign = MAGOT_EXP_TILE_ALIGN;
+constexpr uint64_t kTileAlign = 128;
 constexpr int kPepPerLane = 2;                // residue chunk slots per lane
 constexpr int kHalo = 3 * kChunk;             // look-ahead decoded past the tile: codons of
                                               // the residues rounded up to a 16-byte store
-#ifndef MAGOT_EXP_EXON_CAP
-#define MAGOT_EXP_EXON_CAP 128
-#endif
-constexpr int kExonCap = MAGOT_EXP_EXON_CAP;  // intervals staged in LDS per tile (7 blocks of 4 waves fit a CU's LDS)
+constexpr int kExonCap = 128;  // intervals staged in LDS per tile (7 blocks of 4 waves fit a CU's LDS)
 static_assert((kExonCap & (kExonCap - 1)) == 0, "kExonCap must be a power of two (row index masks)");
 constexpr int kTxCap = 64;                    // records staged in LDS per tile
 constexpr int kPepSlots = 64 * kPepPerLane;  // residue chunks per tile

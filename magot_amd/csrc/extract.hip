@@ -184,10 +184,6 @@ __device__ __forceinline__ uint32_t pack_codes(uint32_t x0, uint32_t x1) {
   return __builtin_amdgcn_perm(z1, z0, 0x06040200u);
 }
 
-#ifndef MAGOT_EXP_LOAD_AUX
-#define MAGOT_EXP_LOAD_AUX 0  // cache-policy bits of the genome window loads
-#endif
-
 // Output store: plain for the 128-byte lines a tile shares with its
 // neighbours (L2 merges the two tiles' halves of such a line), non-temporal
 // elsewhere.  A/B on one box, 200 back-to-back C3 steps: 0.2827 -> 0.2813 ms,
@@ -431,7 +427,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const uint32_t* pla
 }
 
 __device__ __forceinline__ uint3 load_window(__amdgpu_buffer_rsrc_t plane, uint32_t off) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b96(plane, off, 0, MAGOT_EXP_LOAD_AUX);
+  const auto v = __builtin_amdgcn_raw_buffer_load_b96(plane, off, 0, 0);  // default cache policy
   return make_uint3(v[0], v[1], v[2]);
 }
 
@@ -486,10 +482,7 @@ __global__ __launch_bounds__(kThreads) void extract_kernel(ExtractArgs a) {
   // 2 / 4 / 16 / 64 / 256 blocks -0.5 / -0.5 / -0.7 / +0.8 / +5 % per step
   // against round-robin; one contiguous run per XCD +7 %.  Complete groups of
   // 8 runs only, the tail keeps the identity order (a bijection).
-#ifndef MAGOT_EXP_XCD_RUN
-#define MAGOT_EXP_XCD_RUN 16
-#endif
-  constexpr uint32_t kXcdRun = MAGOT_EXP_XCD_RUN;
+  constexpr uint32_t kXcdRun = 16;
   const uint32_t xb = blockIdx.x, grp = xb / (8 * kXcdRun);
   const uint32_t vb = (grp + 1) * 8 * kXcdRun <= gridDim.x
                           ? grp * 8 * kXcdRun + (xb % 8) * kXcdRun + (xb / 8) % kXcdRun : xb;

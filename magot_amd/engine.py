@@ -101,6 +101,43 @@ class DeviceGenome(object):
               'magot_genome_wire_ranges')
         return [(int(off[k]), int(ln[k])) for k in range(n.value)]
 
+    def wire_size(self):
+        """Bytes of the compact replica image (magot_genome_wire_export)."""
+        n = ctypes.c_uint64()
+        check(_lib.lib().magot_genome_wire_export(self.handle, None, 0, ctypes.byref(n)),
+              'magot_genome_wire_export')
+        return n.value
+
+    def wire_export(self, dst_dev_ptr, cap):
+        """Write the compact replica image (2-bit codes, soft-mask runs,
+        exception runs) into caller device memory of ``cap`` bytes; returns
+        its size."""
+        n = ctypes.c_uint64()
+        check(_lib.lib().magot_genome_wire_export(self.handle, ctypes.c_void_p(dst_dev_ptr),
+                                                  int(cap), ctypes.byref(n)),
+              'magot_genome_wire_export')
+        return n.value
+
+    @classmethod
+    def from_wire(cls, meta, wire_dev_ptr, wire_bytes, names, lengths, ctx=None):
+        """A genome rebuilt on this device from a replica image in device
+        memory (magot_genome_wire_import); it owns its arena, and the image
+        can be freed afterwards."""
+        self = cls.__new__(cls)
+        self.ctx = ctx or _lib.default_context()
+        self.names = list(names)
+        self.index = {nm: i for i, nm in enumerate(self.names)}
+        self.lengths = np.asarray(lengths, dtype=np.uint64)
+        self._keepalive = None
+        m = np.frombuffer(meta, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        check(_lib.lib().magot_genome_wire_import(self.ctx.handle, ptr(m), len(m),
+                                                  ctypes.c_void_p(wire_dev_ptr), int(wire_bytes),
+                                                  ctypes.byref(h)), 'magot_genome_wire_import')
+        self.handle = h
+        self._stats()
+        return self
+
     def copy_arena(self, dst_dev_ptr):
         """D2D copy of the packed arena to caller device memory (an address)."""
         check(_lib.lib().magot_genome_copy_arena(self.handle, ctypes.c_void_p(dst_dev_ptr)),

@@ -117,13 +117,36 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
             index = engine.fasta_contigs(fa)  # the same reader as the load
             if index is not None:
                 plan = plan_gff(*index)
-        finally:
+        except BaseException:
+            # the genome may already be on the device: free it before raising
+            try:
+                loaded = loading.result()
+            except Exception:
+                loaded = None
+            if loaded is not None:
+                loaded.close()
+            raise
+        try:
             dev = loading.result()
+        except BaseException:
+            if plan is not None:
+                plan.close()
+            raise
+    owned = dev  # the FastaGenome this call loaded (closed on every return)
     if dev is None and plan is not None:  # above one device plane
         plan.close()
         plan = None
     elif dev is not None and plan is None:
+        dev.close()
         return None, None
+    try:
+        return _gff2fasta_run(genome_sequence, dev, plan, plan_gff)
+    finally:
+        if owned is not None:
+            owned.close()
+
+
+def _gff2fasta_run(genome_sequence, dev, plan, plan_gff):
     seqs = None
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)

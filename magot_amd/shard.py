@@ -3,10 +3,10 @@
 One process per GPU (torchrun); ``torch.distributed`` with the nccl backend is
 RCCL over xGMI on MI355X.  The job:
 
-  1. rank 0 packs the genome once (magot_genome_load) and the packed arena's
-     wire ranges (forward plane, runs, directory) are broadcast device-to-
-     device to every rank (``replicate_genome``); the other ranks attach to
-     the received bytes and rebuild the mirror plane (magot_genome_attach_wire);
+  1. rank 0 packs the genome once (magot_genome_load) and its compact
+     replica image (2-bit codes, soft-mask runs, exception runs) is broadcast
+     device-to-device to every rank (``replicate_genome``); the other ranks
+     rebuild the packed arena from it (magot_genome_wire_import);
   2. records are sharded in genome order into equal-weight ranges
      (``record_shards``: contigs stay whole except where a range boundary
      splits one at a transcript boundary), so a record never spans ranks and
@@ -101,15 +101,23 @@ def collective_device(dist):
 
 
 
-def replicate_genome(dist, rank, contigs, ctx):
+def replicate_genome(dist, rank, contigs, ctx, root_replica=False):
     """The packed genome on every rank: packed once on rank 0, broadcast.
 
-    Only the arena's wire ranges cross the links (the forward nibble plane,
-    the exception runs and their directory: magot_genome_wire_ranges); every
-    receiving rank rebuilds the reverse-strand mirror on its own device
-    (magot_genome_attach_wire), so the broadcast moves half the arena.
+    What crosses the links is the genome's compact replica image
+    (magot_genome_wire_export: the forward strand's 2-bit codes, the
+    soft-masked bases as runs, the exception runs -- about 0.27 B per base
+    against the packed arena's 1 B); every receiving rank rebuilds the nibble
+    plane and its mirror from it on its own device (magot_genome_wire_import)
+    and frees the image.  The genome's meta blob (contig table, exception run
+    list for the planner) goes with the object broadcast.
     ``contigs`` is the (name, sequence) list on rank 0 (ignored elsewhere).
-    Returns (DeviceGenome, seconds spent in the broadcast, bytes broadcast)."""
+    ``root_replica``: rank 0 too continues on a replica rebuilt from the
+    image (its packed original is closed) -- the one-rank job then exercises
+    the receiving side as well.
+    Returns (DeviceGenome, record): seconds of the export, the broadcast
+    (max over ranks is the caller's) and the rebuild, bytes of the image and
+    of the meta blob."""
     import time
 
     import torch
@@ -117,34 +125,43 @@ def replicate_genome(dist, rank, contigs, ctx):
     from . import engine
     if rank == 0:
         dev = engine.DeviceGenome(contigs, ctx=ctx)
-        meta, nbytes = dev.export()
-        info = [meta, nbytes, dev.names, [int(x) for x in dev.lengths], dev.wire_ranges()]
+        meta, _ = dev.export()
+        info = [meta, dev.wire_size(), dev.names, [int(x) for x in dev.lengths]]
     else:
         dev = None
-        info = [None, None, None, None, None]
-    dist.broadcast_object_list(info, src=0)
-    meta, nbytes, names, lengths, ranges = info
+        info = [None, None, None, None]
+    t0 = time.perf_counter()
+    dist.broadcast_object_list(info, src=0)  # the other ranks wait here for rank 0's pack
+    t_meta = time.perf_counter() - t0
+    meta, nbytes, names, lengths = info
     where = collective_device(dist)
-    buf = torch.empty(nbytes, dtype=torch.uint8, device='cuda')
-    if rank == 0:
-        dev.copy_arena(buf.data_ptr())
+    buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device='cuda')
     torch.cuda.synchronize()
+    t_export = 0.0
+    if rank == 0:
+        t0 = time.perf_counter()
+        dev.wire_export(buf.data_ptr(), nbytes)
+        t_export = time.perf_counter() - t0
     dist.barrier()
     t0 = time.perf_counter()
-    for off, ln in ranges:
-        part = buf[off:off + ln]
-        if where == 'cuda':
-            dist.broadcast(part, src=0)
-        else:
-            host = part.cpu()
-            dist.broadcast(host, src=0)
-            part.copy_(host)
+    if where == 'cuda':
+        dist.broadcast(buf, src=0)
+    else:
+        host = buf.cpu()
+        dist.broadcast(host, src=0)
+        buf.copy_(host)
     torch.cuda.synchronize()
     t_bcast = time.perf_counter() - t0
-    if rank != 0:
-        dev = engine.DeviceGenome.attach(meta, buf.data_ptr(), names, lengths, ctx=ctx,
-                                         keepalive=buf, wire=True)
-    return dev, t_bcast, sum(ln for _, ln in ranges)
+    t_import = 0.0
+    if rank != 0 or root_replica:
+        if dev is not None:
+            dev.close()
+        t0 = time.perf_counter()
+        dev = engine.DeviceGenome.from_wire(meta, buf.data_ptr(), nbytes, names, lengths, ctx=ctx)
+        t_import = time.perf_counter() - t0
+    del buf
+    return dev, {'export_s': t_export, 'broadcast_s': t_bcast, 'rebuild_s': t_import,
+                 'image_bytes': int(nbytes), 'meta_bytes': len(meta), 'meta_s': t_meta}
 
 
 class Gather(object):

@@ -13,7 +13,10 @@ point exceptions.  Configs:
   C3  1 Gb, 64 lognormal contigs (sigma 1, min 1 Mb), 500k transcripts,
       1+Poisson(7) exons of U[50,250], introns U[60,5000], strand 50/50
   C5  3 Gb, 200 lognormal contigs, 2M transcripts, exon model of C3
-Seeds: 20261015 + config index.
+Seeds: 20261015 + config index.  Draw order (round 5 on): contig lengths,
+transcripts, then the genome bytes, so the record tables can be made without
+the genome (``make(..., genome=False)``); rounds 1-4 drew the genome before the
+transcripts, so their C2/C3/C5 record sets differ from these.
 """
 
 import numpy as np
@@ -261,11 +264,17 @@ def _sort_by_position(w):
     return w
 
 
-def make(config, seed=None, genome_bases=None, n_tx=None, iupac_rate=None, order='random'):
+def make(config, seed=None, genome_bases=None, n_tx=None, iupac_rate=None, order='random',
+         genome=True):
     """Build a named workload.  ``genome_bases`` / ``n_tx`` rescale it (tests).
     ``order``: 'random' (transcripts in placement order within each contig) or
-    'sorted' (by start coordinate, as a coordinate-sorted GFF)."""
-    w = _make(config, seed, genome_bases, n_tx, iupac_rate)
+    'sorted' (by start coordinate, as a coordinate-sorted GFF).
+    ``genome=False``: the contig lengths and the transcript set only
+    (``Workload.genome`` is None) -- the same tables a full ``make`` returns,
+    since the generator draws the contigs, then the transcripts, then the
+    genome bytes from one stream.  A rank of a multi-GPU job that receives the
+    genome over the collective needs only these."""
+    w = _make(config, seed, genome_bases, n_tx, iupac_rate, genome)
     if order == 'sorted':
         w = _sort_by_position(w)
     elif order != 'random':
@@ -273,7 +282,9 @@ def make(config, seed=None, genome_bases=None, n_tx=None, iupac_rate=None, order
     return w
 
 
-def _make(config, seed, genome_bases, n_tx, iupac_rate):
+def _make(config, seed, genome_bases, n_tx, iupac_rate, with_genome=True):
+    # draw order: contig lengths, transcripts, genome bytes (the tables never
+    # depend on the genome draws, so genome=False skips them)
     idx = {'C2': 2, 'C3': 3, 'C5': 5, 'small': 9}[config]
     rng = np.random.default_rng(SEED_BASE + idx if seed is None else seed)
     if config == 'C2':
@@ -282,12 +293,13 @@ def _make(config, seed, genome_bases, n_tx, iupac_rate):
         n_ctg = 16
         L = np.full(n_ctg, G // n_ctg, dtype=np.int64)
         L[-1] += G - L.sum()
-        genome = _genome(rng, G, iupac_rate=1e-6 if iupac_rate is None else iupac_rate)
         p = L / L.sum()
         tx_contig = np.sort(rng.choice(n_ctg, size=T, p=p))
         ex_len = rng.integers(150, 1851, size=T)
         room = L[tx_contig] - ex_len
         ex_start = (rng.random(T) * room).astype(np.int64)
+        genome = _genome(rng, G, iupac_rate=1e-6 if iupac_rate is None else iupac_rate) \
+            if with_genome else None
         return Workload('C2', genome, L, tx_contig.astype(np.int64), np.ones(T, np.int8),
                         np.ones(T, np.int64), ex_start, ex_len.astype(np.int64), 'nuc')
     if config in ('C3', 'C5', 'small'):
@@ -296,8 +308,8 @@ def _make(config, seed, genome_bases, n_tx, iupac_rate):
         n_ctg = {'C3': 64, 'C5': 200, 'small': 8}[config]
         min_len = min(1_000_000, G // (2 * n_ctg))
         L = _lognormal_contigs(rng, G, n_ctg, min_len)
-        rate = iupac_rate if iupac_rate is not None else (1e-6 if config != 'small' else 1e-3)
-        genome = _genome(rng, G, iupac_rate=rate)
         tx = _transcripts(rng, L, T)
+        rate = iupac_rate if iupac_rate is not None else (1e-6 if config != 'small' else 1e-3)
+        genome = _genome(rng, G, iupac_rate=rate) if with_genome else None
         return Workload(config, genome, L, *tx, outputs='nuc+pep')
     raise ValueError(config)

@@ -25,49 +25,85 @@ from magot_amd import synth  # noqa: E402
 from oracle import magot_oracle as mo  # noqa: E402
 
 
+def _time_loop(fn, min_s=2.0):
+    """Seconds per call of fn(), repeated until min_s has passed."""
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= min_s:
+            return el / n, n
+
+
+def calibrate(ref, name, fa, gff):
+    """One row: the reference's and the port's AnnotationSet.get_fasta('gene')
+    (genome.py:578-582, the gff2fasta loop: every gene's records gathered,
+    nucleotide then protein) on the same FASTA + annotation text, parsed
+    beforehand (parsing is not timed)."""
+    g = ref.Genome(fa)
+    with contextlib.redirect_stdout(io.StringIO()):
+        g.read_gff(gff)
+    aset = mo.load(fa, gff)
+    with contextlib.redirect_stdout(io.StringIO()):
+        text = aset.get_fasta('gene', seq_type='nucleotide')
+    lines = text.split('\n')
+    bases = sum(len(x) for x in lines if not x.startswith('>'))
+    records = sum(1 for x in lines if x.startswith('>'))
+
+    def run_ref():
+        with contextlib.redirect_stdout(io.StringIO()):
+            g.annotations.get_fasta('gene', seq_type='nucleotide')
+            g.annotations.get_fasta('gene', seq_type='protein')
+
+    def run_port():
+        with contextlib.redirect_stdout(io.StringIO()):
+            aset.get_fasta('gene', seq_type='nucleotide')
+            aset.get_fasta('gene', seq_type='protein')
+
+    t_ref, n_ref = _time_loop(run_ref)
+    t_port, n_port = _time_loop(run_port)
+    row = {'workload': name, 'cds_bases': bases, 'records': records,
+           'reference_s': t_ref, 'port_s': t_port, 'repeats': [n_ref, n_port],
+           'reference_bases_per_s': bases / t_ref, 'port_bases_per_s': bases / t_port,
+           'port_over_reference': t_ref / t_port}
+    print(json.dumps(row), flush=True)
+    return row
+
+
 def main():
+    import goldlib
     import make_golden
     ref = make_golden.reference_module()
     rows = []
+    # C1: the reference's own O.biroi subset (BASELINE configs[0])
+    with open(goldlib.path('O.biroi_refseqGenomeSubset.fasta')) as fh:
+        fa = fh.read()
+    with open(goldlib.path('O.biroi_NCBIrefseq_gff3Subset.gff')) as fh:
+        gff = fh.read()
+    rows.append(calibrate(ref, 'C1: O.biroi refseq subset (FASTA + GFF3)', fa, gff))
+    # the reference's Chromosome14 test data, rebuilt from its CDS fixture
+    # (tests/golden/goldlib.rebuild_c14), with its standard GTF
+    with open(goldlib.path('StandardGTF.gtf')) as fh:
+        gtf = fh.read()
+    rows.append(calibrate(ref, 'C14: Chromosome14 (rebuilt) + StandardGTF.gtf',
+                          goldlib.rebuild_c14(), gtf))
     for name, gb, ntx in (('synthetic 2 Mb / 1k tx', 2_000_000, 1000),
                           ('synthetic 10 Mb / 5k tx', 10_000_000, 5000)):
         w = synth.make('small', genome_bases=gb, n_tx=ntx)
-        fa, gff = w.fasta_text(), w.gff3_text()
-        bases = int(w.cds_bases)
-        # reference: Genome + read_gff, then get_fasta per mRNA
-        g = ref.Genome(fa)
-        with contextlib.redirect_stdout(io.StringIO()):
-            g.read_gff(gff)
-        mrnas = list(g.annotations.mRNA.values())
-        t0 = time.perf_counter()
-        with contextlib.redirect_stdout(io.StringIO()):
-            for m in mrnas:
-                m.get_fasta('nucleotide')
-            for m in mrnas:
-                m.get_fasta('protein')
-        t_ref = time.perf_counter() - t0
-        # port: same objects through the oracle restatement
-        aset = mo.load(fa, gff)
-        recs = list(aset.mRNA.values())
-        t0 = time.perf_counter()
-        with contextlib.redirect_stdout(io.StringIO()):
-            for r in recs:
-                mo.get_fasta(r, aset, 'nucleotide')
-            for r in recs:
-                mo.get_fasta(r, aset, 'protein')
-        t_port = time.perf_counter() - t0
-        rows.append({'workload': name, 'cds_bases': bases, 'transcripts': len(mrnas),
-                     'reference_s': t_ref, 'port_s': t_port,
-                     'reference_bases_per_s': bases / t_ref, 'port_bases_per_s': bases / t_port,
-                     'port_over_reference': t_ref / t_port})
-        print(json.dumps(rows[-1]), flush=True)
-    out = {'note': 'single-threaded, build container CPU; extraction only (get_fasta nucleotide '
-                   '+ protein over all mRNA); reference = lib2to3 copy of genome.py',
+        rows.append(calibrate(ref, name, w.fasta_text(), w.gff3_text()))
+    ratios = [r['port_over_reference'] for r in rows]
+    out = {'note': 'single-threaded, build container CPU; extraction only (AnnotationSet.get_fasta'
+                   '(gene) nucleotide + protein, each loop repeated for >= 2 s); reference = '
+                   'lib2to3 copy of genome.py (scripts/calibrate_cpu.py)',
            'rows': rows,
-           'port_over_reference_mean': sum(r['port_over_reference'] for r in rows) / len(rows)}
+           'port_over_reference_mean': sum(ratios) / len(ratios),
+           'port_over_reference_min': min(ratios),
+           'port_over_reference_max': max(ratios)}
     with open(os.path.join(ROOT, 'profiles', 'cpu_calibration.json'), 'w') as fh:
         json.dump(out, fh, indent=1)
-    print('port/reference speed ratio: %.1f' % out['port_over_reference_mean'])
+    print('port/reference speed ratio: %.1f (%.1f - %.1f)'
+          % (out['port_over_reference_mean'], min(ratios), max(ratios)))
 
 
 if __name__ == '__main__':

@@ -10,6 +10,7 @@ export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
 # stages: tests slow bench driver c2 c5 multi multi5 rehearse kt kt5 kt2 pmc traffic e2e smoke
+#         dist dist5 fetchcal gloo8c3 gloo8c5 c4shares pytest:<file>
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
 bash scripts/box_info.sh $OUT/box_before
@@ -17,6 +18,44 @@ has() { [[ " $STAGES " == *" $1 "* ]]; }
 if has tests; then
   timeout -k 10 900 python -u -m pytest tests -m "gpu and not slow" -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -40 $OUT/pytest_gpu.log; exit 1; }
   tail -1 $OUT/pytest_gpu.log
+fi
+for st in $STAGES; do
+  # pytest:<path>[::<test>] -- one test file (or test) under -m gpu
+  if [[ $st == pytest:* ]]; then
+    t=${st#pytest:}; n=$(echo "$t" | tr '/:' '__')
+    timeout -k 10 900 python -u -m pytest "$t" -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_$n.log 2>&1 || { tail -40 $OUT/pytest_$n.log; exit 1; }
+    tail -1 $OUT/pytest_$n.log
+  fi
+done
+if has dist; then
+  # the C3 job through the multi-GPU path at N=1: RCCL process group of one rank
+  NCCL_DEBUG=INFO timeout -k 10 600 python $BENCH --dist --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_dist_c3.json 2> $OUT/dist_c3.err || { tail -30 $OUT/dist_c3.err; exit 1; }
+  cut -c1-600 $OUT/bench_dist_c3.json
+fi
+if has dist5; then
+  NCCL_DEBUG=INFO timeout -k 10 900 python $BENCH --dist --config C5 --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_dist_c5.json 2> $OUT/dist_c5.err || { tail -30 $OUT/dist_c5.err; exit 1; }
+  cut -c1-600 $OUT/bench_dist_c5.json
+fi
+if has fetchcal; then
+  # FETCH_SIZE calibration for 12-byte buffer-load windows (scripts/fetchcal.hip)
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 scripts/fetchcal.hip -o /tmp/fetchcal.bin || exit 1
+  timeout -k 10 120 /tmp/fetchcal.bin > $OUT/fetchcal_plain.jsonl || exit 1
+  rm -rf $OUT/fetchcal_pmc $OUT/fetchcal_kt
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetchcal_pmc -o pmc -- /tmp/fetchcal.bin > $OUT/fetchcal_pmc.jsonl 2> $OUT/fetchcal_pmc.err || { tail -5 $OUT/fetchcal_pmc.err; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum --output-format csv -d $OUT/fetchcal_pmc2 -o pmc -- /tmp/fetchcal.bin > $OUT/fetchcal_pmc2.jsonl 2> $OUT/fetchcal_pmc2.err || { tail -5 $OUT/fetchcal_pmc2.err; }
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/fetchcal_kt -o kt -- /tmp/fetchcal.bin > $OUT/fetchcal_kt.jsonl 2> $OUT/fetchcal_kt.err || { tail -5 $OUT/fetchcal_kt.err; exit 1; }
+  cat $OUT/fetchcal_plain.jsonl
+fi
+for cfg in C3 C5; do
+  if has gloo8${cfg,,}; then
+    # the strong job over 8 ranks sharing this card (gloo, device tensors as under nccl)
+    MAGOT_DIST_BACKEND=gloo MAGOT_COLLECTIVE_TENSORS=cuda timeout -k 10 900 python $BENCH --gpus 8 --config $cfg --steps 20 --warmup 5 --no-cpu-baseline > $OUT/bench_gloo8_$cfg.json 2> $OUT/gloo8_$cfg.err || { tail -30 $OUT/gloo8_$cfg.err; exit 1; }
+    grep '^{' $OUT/bench_gloo8_$cfg.json | cut -c1-300
+  fi
+done
+if has c4shares; then
+  timeout -k 10 600 python scripts/c4_shares.py > $OUT/c4_shares.json 2> $OUT/c4_shares.err || { tail -20 $OUT/c4_shares.err; exit 1; }
+  tail -8 $OUT/c4_shares.err
 fi
 if has slow; then
   timeout -k 10 900 python -u -m pytest tests -m "gpu and slow" -q --timeout 600 --timeout-method thread > $OUT/pytest_gpu_slow.log 2>&1 || { tail -40 $OUT/pytest_gpu_slow.log; exit 1; }

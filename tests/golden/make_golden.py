@@ -27,7 +27,8 @@ Outputs (data only: inputs, expected outputs, hashes):
 
 Usage:  python tests/golden/make_golden.py [--only-translate-lib | --only-flank-edges |
                                            --only-fuzz3 | --only-cds2pep2 |
-                                           --only-blast-fuzz | --only-coords-fuzz]
+                                           --only-blast-fuzz | --only-coords-fuzz |
+                                           --only-synth]
 """
 
 import contextlib
@@ -895,6 +896,10 @@ def main():
     with open(os.path.join(HERE, 'translate_lib.json'), 'w') as fh:
         json.dump(make_translate_lib(ref), fh, indent=0, sort_keys=True)
     if '--only-translate-lib' in sys.argv:
+        return
+    if '--only-synth' in sys.argv:
+        with open(os.path.join(HERE, 'synth_small.json'), 'w') as fh:
+            json.dump(make_synth(ref), fh, indent=1, sort_keys=True)
         return
     if '--only-coords-fuzz' in sys.argv:
         with open(os.path.join(HERE, 'coords_fuzz.json'), 'w') as fh:

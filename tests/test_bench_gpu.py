@@ -20,7 +20,8 @@ pytestmark = pytest.mark.gpu
 
 def _bench(args, env_extra=None):
     env = dict(os.environ)
-    env.pop('WORLD_SIZE', None)
+    for k in ('WORLD_SIZE', 'MAGOT_DIST_BACKEND', 'MAGOT_COLLECTIVE_TENSORS'):
+        env.pop(k, None)
     env.update(env_extra or {})
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env,
                        capture_output=True, text=True, timeout=300)
@@ -96,3 +97,22 @@ def test_bench_six_frame_job_two_ranks(tensors):
     g = d['outputs_gather']
     assert g['outputs'] == ['six-frame residues']
     assert g['parity'].startswith('bit-exact') and 'six frames' in g['parity'], g
+
+
+@pytest.mark.parametrize('config', ['small', 'small5'])
+def test_bench_dist_one_rank_rccl(config):
+    """The multi-GPU job's collective path through RCCL itself (nccl backend,
+    a process group of one rank on this card): the genome broadcast out of
+    the wire image and the replica rebuilt from it, the output gather into
+    the rank-major buffer, the reassembly on the device, the float64
+    reductions -- checked bit-exact in global record order."""
+    d = _bench(['--dist', '--config', config] + COMMON)
+    assert d['config']['backend'] == 'nccl', d['config']
+    assert d['n_gpus'] == 1
+    g = d['outputs_gather']
+    assert g['backend'] == 'nccl' and g['collective_tensors'] == 'cuda'
+    assert g['parity'].startswith('bit-exact') and 'global record order' in g['parity'], g
+    assert d['parity'] == g['parity']
+    # the 2-bit replica image (+ meta), not the 1-byte-per-base arena
+    assert d['genome_broadcast_bytes'] < 0.35 * d['genome_arena_bytes'], d['genome_replica']
+    assert d['roofline']['kernel'] == ('orf6_kernel' if config == 'small5' else 'extract_kernel')

@@ -7,6 +7,10 @@
 * the wire replica (magot_genome_wire_ranges + magot_genome_attach_wire):
   only the forward plane, runs and directory are transferred, the mirror is
   rebuilt, and the attached arena equals the packed one byte for byte;
+* the compact replica image (magot_genome_wire_export / _import: 2-bit
+  codes, soft-mask runs, exception runs): the genome rebuilt from it equals
+  the packed arena byte for byte, over every byte value, case patterns that
+  stress the mask runs and directories, edge genomes and C3 / C5;
 * magot_copy_segments against numpy, aligned and unaligned.
 """
 
@@ -186,6 +190,135 @@ def test_wire_replica_c3_genome():
     finally:
         rep.close()
         g.close()
+
+
+def _image_replica(g, poison=0xAB):
+    """What a receiving rank builds: the image written into fresh (poisoned)
+    device memory, a genome imported from it, the image freed."""
+    meta, _ = g.export()
+    n = g.wire_size()
+    buf = torch.full((n + 64,), poison, dtype=torch.uint8, device='cuda')
+    torch.cuda.synchronize()
+    assert g.wire_export(buf.data_ptr(), n) == n
+    rep = engine.DeviceGenome.from_wire(meta, buf.data_ptr(), n, g.names, g.lengths)
+    del buf
+    torch.cuda.synchronize()
+    return rep, n
+
+
+def _assert_image_round_trip(contigs, max_frac=None):
+    g = engine.DeviceGenome(contigs)
+    rep, n = _image_replica(g)
+    try:
+        assert rep.export() == g.export()
+        a, b = _defined(g, _arena(g)), _defined(rep, _arena(rep))
+        if not np.array_equal(a, b):
+            bad = int(np.nonzero(a != b)[0][0])
+            raise AssertionError('rebuilt arena differs at defined byte %d: %r vs %r'
+                                 % (bad, b[bad:bad + 8], a[bad:bad + 8]))
+        if max_frac is not None:
+            assert n < max_frac * g.device_bytes, (n, g.device_bytes)
+        return g.device_bytes, n
+    finally:
+        rep.close()
+        g.close()
+
+
+def _case_genome(kind, rng):
+    acgt = np.frombuffer(b'ACGTacgt', np.uint8)
+    if kind == 'alternating_case':   # a mask run every other base: the densest run list
+        s = np.frombuffer(b'ACGT', np.uint8)[rng.integers(0, 4, 300_000)].copy()
+        s[1::2] |= 0x20
+        return [('a', s.tobytes()), ('b', s[:77].tobytes())]
+    if kind == 'all_lower':          # one mask run across many directory blocks
+        return [('a', b'acgt' * 50_000), ('b', b'ttt'), ('c', b'a' * 8191)]
+    if kind == 'mixed':              # mask runs cut by exceptions (n, N, IUPAC, '-')
+        parts = []
+        for _ in range(4000):
+            k = int(rng.integers(0, 5))
+            ln = int(rng.integers(1, 70))
+            if k == 0:
+                parts.append(rng.choice(acgt[4:], ln))
+            elif k == 1:
+                parts.append(rng.choice(acgt[:4], ln))
+            else:
+                parts.append(np.full(ln, rng.choice(np.frombuffer(b'nNRy-x*', np.uint8)),
+                                     dtype=np.uint8))
+        s = np.concatenate(parts).tobytes()
+        return [('a', s[:len(s) // 3]), ('e', b''), ('b', s[len(s) // 3:])]
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize('kind', ['alternating_case', 'all_lower', 'mixed'])
+def test_image_round_trip_case_patterns(kind):
+    _assert_image_round_trip(_case_genome(kind, np.random.default_rng(41)))
+
+
+def test_image_round_trip_every_byte_value():
+    rng = np.random.default_rng(5)
+    values = [b for b in range(256) if b not in (10, 13)]
+    parts = []
+    for k, b in enumerate(values * 3):
+        parts.append(rng.choice(np.frombuffer(b'ACGTacgt', np.uint8), int(rng.integers(0, 40))))
+        parts.append(np.full(1 + (k * 7) % 45, b, dtype=np.uint8))
+    seq = np.concatenate(parts).tobytes()
+    _assert_image_round_trip([('a', seq[:5000]), ('b', seq[5000:])])
+
+
+@pytest.mark.parametrize('shape', ['empty', 'one_base', 'all_N', 'exc_at_ends'])
+def test_image_round_trip_edge_genomes(shape):
+    contigs = {
+        'empty': [],
+        'one_base': [('a', b'n')],
+        'all_N': [('a', b'N' * 100_000), ('b', b'N' * 33)],
+        'exc_at_ends': [('a', b'RACGTY'), ('b', b'YY' + b'acgt' * 40 + b'-'), ('c', b'')],
+    }[shape]
+    _assert_image_round_trip(contigs)
+
+
+def test_image_replica_extracts_the_same_bytes():
+    w = synth.make('small', seed=12, genome_bases=2_000_000, n_tx=800, iupac_rate=1e-3)
+    g = engine.DeviceGenome(w.contigs())
+    rep, n = _image_replica(g)
+    try:
+        assert n < 0.3 * g.device_bytes
+        ex, tx = w.plan_tables()
+        outs = []
+        for gen in (g, rep):
+            plan = engine.ExtractionPlan(gen, ex, tx)
+            outs.append(plan.run())
+            plan.close()
+        for x, y in zip(outs[0], outs[1]):
+            assert np.array_equal(x, y)
+    finally:
+        rep.close()
+        g.close()
+
+
+def test_image_refused_for_another_genome():
+    a = engine.DeviceGenome([('a', b'ACGTacgtNN' * 1000)])
+    b = engine.DeviceGenome([('a', b'ACGTacgtNN' * 1001)])
+    try:
+        meta_b, _ = b.export()
+        n = a.wire_size()
+        buf = torch.empty(n, dtype=torch.uint8, device='cuda')
+        a.wire_export(buf.data_ptr(), n)
+        with pytest.raises(engine.MagotError):
+            engine.DeviceGenome.from_wire(meta_b, buf.data_ptr(), n, b.names, b.lengths)
+        with pytest.raises(engine.MagotError):   # too small a buffer for the export
+            a.wire_export(buf.data_ptr(), n - 1)
+    finally:
+        a.close()
+        b.close()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize('config', ['C3', 'C5'])
+def test_image_round_trip_full_size(config):
+    """The images a C4 / C5 job broadcasts: 0.27 B per base of the arena's 1 B."""
+    w = synth.make(config)
+    arena, n = _assert_image_round_trip(w.contigs(), max_frac=0.3)
+    print('%s: image %d bytes of a %d-byte arena (%.3f)' % (config, n, arena, n / arena))
 
 
 @pytest.mark.parametrize('aligned', [False, True])
