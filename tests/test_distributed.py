@@ -78,6 +78,68 @@ def test_shard_seed_deterministic():
     assert np.array_equal(a.genome, b.genome) and np.array_equal(a.ex_start, b.ex_start)
 
 
+def test_tables_without_genome_match_full_workload():
+    """Ranks > 0 of a shared job make only the record tables
+    (synth.make(genome=False)): the same contigs, records and intervals as
+    rank 0's full workload, for every configuration shape."""
+    from magot_amd import synth
+    for cfg, kw in (('small', {}), ('C2', {'genome_bases': 400_000, 'n_tx': 300}),
+                    ('C3', {'genome_bases': 2_000_000, 'n_tx': 400})):
+        full = synth.make(cfg, **kw)
+        tab = synth.make(cfg, genome=False, **kw)
+        assert tab.genome is None and full.genome is not None
+        for k in ('contig_len', 'tx_contig', 'tx_strand', 'ex_count', 'ex_start', 'ex_len'):
+            assert np.array_equal(getattr(full, k), getattr(tab, k)), (cfg, k)
+        a, b = full.plan_tables(), tab.plan_tables()
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def _values_worker(rank, world, port, q):
+    os.environ.update({'RANK': str(rank), 'LOCAL_RANK': str(rank), 'WORLD_SIZE': str(world),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
+    import bench
+    dist, r, local, n = bench.dist_setup()
+    vals = bench.all_values(dist, 10.0 * (rank + 1))
+    q.put((rank, vals))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_all_values_two_ranks_gloo():
+    """The per-rank host figures of the line (RSS, set-up) gathered from every rank."""
+    world = 2
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_values_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1] == [10.0, 20.0]
+
+
+def test_dist_setup_one_rank_forced_gloo(tmp_path):
+    """--dist: a process group of one rank (gloo here; nccl = RCCL on a GPU box)."""
+    import subprocess
+    code = ('import os, sys; sys.path.insert(0, %r); import bench; '
+            'os.environ.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", '
+            'MASTER_ADDR="127.0.0.1", MASTER_PORT=str(bench._free_port())); '
+            'd, r, l, n = bench.dist_setup(force=True); '
+            'assert d is not None and n == 1 and d.get_world_size() == 1; '
+            'assert bench.all_values(d, 3.5) == [3.5]; '
+            'assert bench.allreduce_max(d, 2.0) == 2.0; '
+            'print(d.get_backend()); d.destroy_process_group()' % ROOT)
+    env = dict(os.environ)
+    env.pop('WORLD_SIZE', None)
+    r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines()[-1] == 'gloo'
+
+
 # ---------------------------------------------------------------------------
 # C4 (strong) orchestration: magot_amd/shard.py
 # ---------------------------------------------------------------------------
