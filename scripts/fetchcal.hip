@@ -16,6 +16,8 @@
 //   cal_line_hi    ... inside its second 64 bytes
 //   cal_line_cross ... straddling the two 64-byte halves (offset 58)
 //   cal_line_pair  two windows in every 3rd line, one in each half
+//   cal_b64_stream / cal_b64_line  the same with orf6_kernel's 8-byte
+//                  buffer_load_dwordx2 windows (code plane staging)
 // Run it under `rocprofv3 --pmc FETCH_SIZE` (and separately under
 // --kernel-trace --stats); scripts/fetchcal_summary.py divides each kernel's
 // FETCH_SIZE by its known bytes and lines.
@@ -47,7 +49,13 @@ __device__ __forceinline__ uint32_t win(__amdgpu_buffer_rsrc_t r, uint32_t off) 
   return v[0] ^ v[1] ^ v[2];
 }
 
-// mode: 0 stream12, 1 overlap8, 2 line_any, 3 line_lo, 4 line_hi, 5 line_cross, 6 line_pair
+__device__ __forceinline__ uint32_t win8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return v[0] ^ v[1];
+}
+
+// mode: 0 stream12, 1 overlap8, 2 line_any, 3 line_lo, 4 line_hi, 5 line_cross, 6 line_pair,
+//       7 b64 stream, 8 b64 one per 3rd line
 template <int kMode>
 __global__ __launch_bounds__(256) void cal(const uint8_t* base, uint64_t n, uint32_t* sink) {
   const __amdgpu_buffer_rsrc_t r = rsrc(base);
@@ -58,6 +66,11 @@ __global__ __launch_bounds__(256) void cal(const uint8_t* base, uint64_t n, uint
     acc = win(r, (uint32_t)(12 * i));
   } else if (kMode == 1) {
     acc = win(r, (uint32_t)(8 * i));
+  } else if (kMode == 7) {
+    acc = win8(r, (uint32_t)(8 * i));
+  } else if (kMode == 8) {
+    const uint32_t h = (uint32_t)((i * 2654435761ull) >> 7);
+    acc = win8(r, (uint32_t)(3 * i) * 128 + 8 * (h % 16));
   } else {
     const uint32_t line = (uint32_t)(3 * i);
     const uint32_t h = (uint32_t)((i * 2654435761ull) >> 7);
@@ -102,10 +115,10 @@ int main() {
   uint8_t* buf = nullptr;
   uint32_t* sink = nullptr;
   uint4* fl = nullptr;
-  CK(hipMalloc(&buf, 7 * kRegion));
+  CK(hipMalloc(&buf, 9 * kRegion));
   CK(hipMalloc(&fl, kRegion));
   CK(hipMalloc(&sink, 4));
-  CK(hipMemset(buf, 0x5A, 7 * kRegion));
+  CK(hipMemset(buf, 0x5A, 9 * kRegion));
   CK(hipDeviceSynchronize());
   const uint64_t nl = kLines / 3;  // every 3rd line
   run<0>("cal_stream12", buf + 0 * kRegion, kRegion / 12, kRegion / 12 * 12, kLines, fl, sink);
@@ -115,6 +128,8 @@ int main() {
   run<4>("cal_line_hi", buf + 4 * kRegion, nl, nl * 12, nl, fl, sink);
   run<5>("cal_line_cross", buf + 5 * kRegion, nl, nl * 12, nl, fl, sink);
   run<6>("cal_line_pair", buf + 6 * kRegion, nl, nl * 24, nl, fl, sink);
+  run<7>("cal_b64_stream", buf + 7 * kRegion, kRegion / 8, kRegion, kLines, fl, sink);
+  run<8>("cal_b64_line", buf + 8 * kRegion, nl, nl * 8, nl, fl, sink);
   CK(hipDeviceSynchronize());
   return 0;
 }
