@@ -38,7 +38,8 @@ def main(d, config, kernel):
         'tcc_ea_wrreq': mean.get('TCC_EA0_WRREQ'),
         'correction': 'FETCH_SIZE x2 (gfx950 128-B fills tallied at 64 B), WRITE_SIZE x1',
         'calibration': 'x2 calibrated for these kernels\' own loads (round 5, '
-                       'profiles/r05/fetchcal.json): 12-byte buffer_load_dwordx3 windows, '
+                       'profiles/r05/fetchcal.json): 12-byte buffer_load_dwordx3 windows '
+                       '(extract_kernel) and 8-byte buffer_load_dwordx2 windows (orf6_kernel), '
                        'streaming or one per line anywhere in it, cost one TCC_EA0_RDREQ per '
                        '128-B line and FETCH_SIZE tallies 64 B per request; fabric reads '
                        'include Infinity Cache hits (an upper bound on HBM reads)',
