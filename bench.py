@@ -198,8 +198,9 @@ def settle(fn, sync, ms):
     launches), before the W warm-up steps.  After an idle period (the parity
     check keeps the GPU idle for seconds) the first ~30 back-to-back C3 launches
     of a fresh box swing 0.274 -> 0.328 -> 0.279 ms over ~12 ms
-    (profiles/r02_settle/launch_order.txt); the timed steps measure the steady
-    state after it.  Reported in the JSON line as `settle`."""
+    (r02_settle/launch_order.txt in profiles/archive_r01_r04.tar.xz); the timed
+    steps measure the steady state after it.  Reported in the JSON line as
+    `settle`."""
     n = 0
     t0 = time.perf_counter()
     while True:
@@ -837,8 +838,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     # C3 kernel durations drift by up to 15 % over the first few dozen launches
-    # on a fresh box (profiles/r01_v13/kt_launch_order.txt); 20 untimed warm-up steps
-    # and 100 timed ones (about 30 ms of C3 work) measure the steady state.
+    # on a fresh box (r01_v13/kt_launch_order.txt, profiles/archive_r01_r04.tar.xz);
+    # 20 untimed warm-up steps and 100 timed ones (about 30 ms of C3 work) measure
+    # the steady state.
     ap.add_argument('--steps', type=int, default=100)
     ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--settle-ms', type=float, default=100.0,

@@ -2,7 +2,8 @@
 process on one box: round 5 draws the record tables before the genome bytes
 (synth.py); round 4 drew the genome first, so the same seed gives another
 (identically distributed) record set.  Times back-to-back launches of both
-plans, alternating.
+plans, alternating, and of both with the class-7 IUPAC bytes (S, W) replaced by
+classed ones (R, Y), which moves their intervals off the run-list path.
 
     python scripts/c2_draw_order.py > profiles/r05/c2_draw_order.json
 """
@@ -40,8 +41,19 @@ def main():
     res = {}
     plans = {}
     gens = []
-    for name, w in (('round5_order', synth.make('C2')), ('round4_order', round4_c2(seed))):
-        dev = engine.DeviceGenome(w.contig_views(), ctx=ctx)
+    w5, w4 = synth.make('C2'), round4_c2(seed)
+    cases = [('round5_order', w5, w5.genome), ('round4_order', w4, w4.genome)]
+    # the same two with the class-7 IUPAC bytes (S, W: no literal class, the
+    # run-list path) mapped to classed ones (R, Y)
+    for name, w in (('round5_order_no_class7', w5), ('round4_order_no_class7', w4)):
+        g = w.genome.copy()
+        g[g == ord('S')] = ord('R')
+        g[g == ord('W')] = ord('Y')
+        cases.append((name, w, g))
+    for name, w, genome in cases:
+        contigs = [(w.contig_names[i], genome[w.contig_off[i]:w.contig_off[i + 1]])
+                   for i in range(len(w.contig_len))]
+        dev = engine.DeviceGenome(contigs, ctx=ctx)
         gens.append(dev)
         plans[name] = engine.ExtractionPlan(dev, *w.plan_tables(), engine.OUT_NUC)
         res[name] = {'cds_bases': int(w.cds_bases), 'ms': [],

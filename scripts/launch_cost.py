@@ -44,6 +44,8 @@ def main():
     if a.trace:
         print(json.dumps(trace_summary(a.trace), indent=1))
         return
+    import torch  # before libmagot: torch brings its own HIP runtime (bench.py's order)
+
     from magot_amd import _lib, engine, synth
     w = synth.make('small', seed=5, genome_bases=2_000_000, n_tx=400)
     ctx = _lib.Context(0)
@@ -60,7 +62,6 @@ def main():
     dev.close()
     # a minimal kernel for scale: torch's one-element add_, back to back inside
     # one captured graph (no Python between the launches)
-    import torch
     x = torch.zeros(1, device='cuda')
     side = torch.cuda.Stream()
     with torch.cuda.stream(side):

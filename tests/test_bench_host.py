@@ -1,16 +1,14 @@
 """bench.py's host-side record keeping, on CPU: the amd-smi fields of the box
-record (parsed from a metric dump a GPU box wrote, profiles/r03_close4) and
+record (parsed from a metric dump a GPU box wrote in round 3, kept as
+tests/data/amd_smi_metric_r03.txt) and
 the counter deltas over the timed region."""
 import os
 import re
 
-import pytest
-
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DUMP = os.path.join(ROOT, 'profiles', 'r03_close4', 'box', 'box_before', 'metric.txt')
+DUMP = os.path.join(ROOT, 'tests', 'data', 'amd_smi_metric_r03.txt')
 
 
-@pytest.mark.skipif(not os.path.exists(DUMP), reason='no amd-smi dump in profiles/')
 def test_smi_fields_parse_a_real_dump():
     import bench
     text = open(DUMP).read()
