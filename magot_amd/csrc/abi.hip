@@ -1095,6 +1095,25 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     return MAGOT_ERR_ARG;
   }
   const uint32_t n_tiles = (uint32_t)n_tiles64;
+  // Launch order: tiles that may take the run-list path first -- a staged
+  // interval over a byte without a literal class (kSlowLitBit), or one short
+  // enough that a chunk can span three intervals.  Their chains of dependent
+  // run-list loads then overlap the rest of the launch; at the end of the grid
+  // they set its tail (C2: 0.0174 ms with the 23 such tiles where they fall,
+  // 0.0151 ms with none).  Every other tile keeps output order.
+  std::vector<TileRec> tiles(n_tiles);
+  std::vector<TileRec> tail;
+  uint32_t n_first = 0;
+  for (uint32_t t = 0; t < n_tiles; ++t) {
+    const TileRec r{tile_start[t], tile_start[t + 1], tile_q[t], tile_q[t + 1],
+                    tile_ex[2 * t], tile_ex[2 * t + 1], tile_tx[2 * t], tile_tx[2 * t + 1]};
+    bool slow = false;
+    for (uint32_t e = r.e1; e < r.e2 && !slow; ++e)
+      slow = (ex_g[e] & kSlowLitBit) || ex_out[e + 1] - ex_out[e] < (uint64_t)kChunk;
+    if (slow) tiles[n_first++] = r;
+    else tail.push_back(r);
+  }
+  std::copy(tail.begin(), tail.end(), tiles.begin() + n_first);
 
   // --- device arena -----------------------------------------------------------
   std::unique_ptr<magot_plan> p(new magot_plan());
@@ -1110,10 +1129,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   const uint64_t o_exo = cv.take<uint64_t>(Ec + 2);
   const uint64_t o_txn = cv.take<uint64_t>(Tc + 2);
   const uint64_t o_txp = cv.take<uint64_t>(Tc + 2);
-  const uint64_t o_ts = cv.take<uint64_t>(tile_start.size());
-  const uint64_t o_tex = cv.take<uint32_t>(tile_ex.size() + 2);
-  const uint64_t o_ttx = cv.take<uint32_t>(tile_tx.size() + 2);
-  const uint64_t o_tq = cv.take<uint64_t>(tile_q.size());
+  const uint64_t o_tiles = cv.take<TileRec>(n_tiles + 1);
   const uint64_t o_nuc = cv.take<uint8_t>((outputs & MAGOT_OUT_NUC) ? B + 64 : 64);
   const uint64_t o_pep = cv.take<uint8_t>((outputs & MAGOT_OUT_PEP) ? P + 64 : 64);
   MAGOT_HIP_TRY(hipMalloc(&p->arena, cv.used));
@@ -1127,10 +1143,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   MAGOT_HIP_TRY(up(o_exo, ex_out.data(), (Ec + 2) * 8));
   MAGOT_HIP_TRY(up(o_txn, tn.data(), (Tc + 2) * 8));
   MAGOT_HIP_TRY(up(o_txp, tp.data(), (Tc + 2) * 8));
-  MAGOT_HIP_TRY(up(o_ts, tile_start.data(), tile_start.size() * 8));
-  MAGOT_HIP_TRY(up(o_tex, tile_ex.data(), tile_ex.size() * 4));
-  MAGOT_HIP_TRY(up(o_ttx, tile_tx.data(), tile_tx.size() * 4));
-  MAGOT_HIP_TRY(up(o_tq, tile_q.data(), tile_q.size() * 8));
+  MAGOT_HIP_TRY(up(o_tiles, tiles.data(), tiles.size() * sizeof(TileRec)));
 
   ExtractArgs& a = p->args;
   a.nib = g->nib;
@@ -1141,10 +1154,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   a.ex_out = reinterpret_cast<const uint64_t*>(base + o_exo);
   a.tx_nuc = reinterpret_cast<const uint64_t*>(base + o_txn);
   a.tx_pep = reinterpret_cast<const uint64_t*>(base + o_txp);
-  a.tile_start = reinterpret_cast<const uint64_t*>(base + o_ts);
-  a.tile_ex = reinterpret_cast<const uint32_t*>(base + o_tex);
-  a.tile_tx = reinterpret_cast<const uint32_t*>(base + o_ttx);
-  a.tile_q = reinterpret_cast<const uint64_t*>(base + o_tq);
+  a.tiles = reinterpret_cast<const TileRec*>(base + o_tiles);
   a.nuc = reinterpret_cast<uint8_t*>(base + o_nuc);
   a.pep = reinterpret_cast<uint8_t*>(base + o_pep);
   a.total_nuc = B;

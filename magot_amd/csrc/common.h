@@ -187,6 +187,17 @@ __device__ __forceinline__ void store16(uint8_t* dst, uint4 v) {
 constexpr uint32_t kDebugSlowNuc = 1u << 8;
 constexpr uint32_t kDebugSlowPep = 1u << 9;
 
+// One extraction tile (a wave's work): nucleotide output bytes [T0, T1),
+// residues [Q0, Q1), staged intervals [e1, e2) and records [j1, j2).  Tiles
+// are stored in launch order, which is not output order: tiles that may take
+// the run-list path go first (magot_plan_create), so their extra dependent
+// loads overlap the rest of the launch instead of extending its tail.
+struct TileRec {
+  uint64_t T0, T1, Q0, Q1;
+  uint32_t e1, e2, j1, j2;
+};
+static_assert(sizeof(TileRec) == 48, "TileRec is 48 bytes");
+
 // Device plan.  Zero-length intervals and records without a codon are
 // compacted away on the host (they add no output); tiles are 16-byte aligned
 // ranges of the nucleotide output of at most tile_bytes(lane_chunks) bytes, cut shorter where
@@ -202,10 +213,7 @@ struct ExtractArgs {
   const uint64_t* ex_out;     // n+1 output prefix offsets
   const uint64_t* tx_nuc;     // per codon-bearing record: output start (n+1, sentinel B)
   const uint64_t* tx_pep;     // per codon-bearing record: residue start (n+1, sentinel P)
-  const uint64_t* tile_start; // n_tiles+1
-  const uint32_t* tile_ex;    // 2 per tile: [first interval, end)
-  const uint32_t* tile_tx;    // 2 per tile: [first record, end)
-  const uint64_t* tile_q;     // n_tiles+1: first residue whose codon starts in the tile
+  const TileRec* tiles;       // n_tiles, in launch order
   uint8_t* nuc;
   uint8_t* pep;
   uint64_t total_nuc;

@@ -291,15 +291,17 @@ __device__ __forceinline__ T sload(const T* p, uint32_t i) {
 }
 
 __device__ __forceinline__ TileDesc load_desc(const ExtractArgs& a, uint32_t t) {
+  typedef const __attribute__((address_space(4))) TileRec CT;
+  CT* r = (CT*)a.tiles + t;  // one round of scalar loads (48 bytes)
   TileDesc d;
-  d.T0 = sload(a.tile_start, t);
-  d.T1 = sload(a.tile_start, t + 1);
-  d.Q0 = sload(a.tile_q, t);
-  d.Q1 = sload(a.tile_q, t + 1);
-  d.eb = sload(a.tile_ex, 2 * t);
-  d.m = sload(a.tile_ex, 2 * t + 1) - d.eb;
-  d.tb = sload(a.tile_tx, 2 * t);
-  d.nt = sload(a.tile_tx, 2 * t + 1) - d.tb;
+  d.T0 = r->T0;
+  d.T1 = r->T1;
+  d.Q0 = r->Q0;
+  d.Q1 = r->Q1;
+  d.eb = r->e1;
+  d.m = r->e2 - r->e1;
+  d.tb = r->j1;
+  d.nt = r->j2 - r->j1;
   return d;
 }
 
