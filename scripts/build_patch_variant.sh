@@ -16,9 +16,13 @@ cp -r magot_amd include $W/
 ROOT=$(pwd)
 for p in "${PATCHES[@]}"; do (cd $W && patch -p1 -s < "$ROOT/$p"); done
 objs=""
+hdr=0  # a changed header recompiles every translation unit
+for h in $W/magot_amd/csrc/*.h $W/include/*.h; do
+  cmp -s $h ${h#$W/} || hdr=1
+done
 for s in $W/magot_amd/csrc/*.hip $W/magot_amd/csrc/*.cpp; do
   b=$(basename $s)
-  if ! cmp -s $s magot_amd/csrc/$b || [ ${#FLAGS[@]} -gt 0 ]; then
+  if [ $hdr = 1 ] || ! cmp -s $s magot_amd/csrc/$b || [ ${#FLAGS[@]} -gt 0 ]; then
     lang=""; [[ $b == *.hip ]] && lang="-x hip"
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wno-unused-function --offload-arch=gfx950 -I$W/include "${FLAGS[@]}" $lang -c $s -o $W/$b.o
     objs="$objs $W/$b.o"
