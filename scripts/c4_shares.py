@@ -1,5 +1,6 @@
 """The C4 job's per-GPU shares timed on ONE box, in ONE process (VERDICT r4
-item 5): the full C3 job and every shard of the N = 2, 4 and 8 splits
+item 5): the full C3 job (or, --config C5, the six-frame job) and every
+shard of the N = 2, 4 and 8 splits
 (bench.py's strong-mode sharding, shard.record_shards) are planned over one
 packed genome and timed in alternating rounds, so each projected speed-up
 (full job / slowest shard) is a same-box, same-process ratio.
@@ -36,18 +37,27 @@ def main():
     first = np.zeros(w.n_tx + 1, dtype=np.int64)
     np.cumsum(w.ex_count, out=first[1:])
     tx_bases = np.add.reduceat(w.ex_len, first[:-1])
-    outputs = engine.OUT_NUC | engine.OUT_PEP
-    plans = {'full': engine.ExtractionPlan(dev, *w.plan_tables(), outputs)}
+    c5 = a.config == 'C5'
+    outputs = engine.OUT_NUC if c5 else engine.OUT_NUC | engine.OUT_PEP
+    keep = []
+
+    def make_plan(tables):
+        """The timed object: the extraction plan (C3), or its six-frame plan (C5)."""
+        p = engine.ExtractionPlan(dev, *tables, outputs)
+        if not c5:
+            return p
+        keep.append(p)
+        return engine.Orf6Plan(p)
+
+    plans = {'full': make_plan(w.plan_tables())}
     loads = {}
     for n in (2, 4, 8):
         shards, load, _ = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), n,
                                               tx_start=w.ex_start[first[:-1]])
         loads[n] = load.tolist()
         for r, sh in enumerate(shards):
-            plans['%d:%d' % (n, r)] = engine.ExtractionPlan(dev, *w.plan_tables(tx_subset=sh),
-                                                            outputs)
-    plans['one_record'] = engine.ExtractionPlan(dev, *w.plan_tables(tx_subset=np.array([0])),
-                                                outputs)
+            plans['%d:%d' % (n, r)] = make_plan(w.plan_tables(tx_subset=sh))
+    plans['one_record'] = make_plan(w.plan_tables(tx_subset=np.array([0])))
     sys.stderr.write('planned %d plans in %.1fs\n' % (len(plans), time.perf_counter() - t0))
     for p in plans.values():  # warm every plan once
         p.time_b2b(20)
@@ -61,9 +71,11 @@ def main():
     info = ctx.info()
     res = {'config': a.config, 'rounds': a.rounds, 'launches_per_timing': a.launches,
            'device': info,
-           'plans': {k: {'ms': v, 'bytes_out': int(plans[k].nuc_bytes + plans[k].pep_bytes),
-                         'algorithmic_bytes': plans[k].algorithmic_bytes,
-                         'records': int(plans[k].n_tx)}
+           'kernel': 'orf6_kernel' if c5 else 'extract_kernel',
+           'plans': {k: {'ms': v,
+                         'bytes_out': int(plans[k].total if c5
+                                          else plans[k].nuc_bytes + plans[k].pep_bytes),
+                         'records': int(plans[k].plan.n_tx if c5 else plans[k].n_tx)}
                      for k, v in times.items()},
            'shard_loads': loads}
     proj = {}
@@ -81,7 +93,7 @@ def main():
                    '(genome broadcast, output gather) are outside the step as in bench.py')
     json.dump(res, sys.stdout, indent=1)
     sys.stdout.write('\n')
-    for p in plans.values():
+    for p in list(plans.values()) + keep:
         p.close()
     dev.close()
 
