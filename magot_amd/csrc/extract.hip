@@ -747,17 +747,14 @@ void launch_mirror_planes(uint32_t* nib, uint64_t span, hipStream_t s) {
 // memory system it is bound by.  A/B on one box, 3 alternating runs of the
 // default bench: 0.2729 / 0.2730 / 0.2728 ms per step at 6 blocks against
 // 0.2761 / 0.2761 / 0.2763 at 7 (5 blocks: 0.2749 / 0.2754 / 0.2762).  The cap
-// is dynamic LDS that the kernel never touches; MAGOT_EXTRACT_BLOCKS_PER_CU
-// overrides it (0: no cap).
+// is dynamic LDS that the kernel never touches (an override for occupancy
+// sweeps: scripts/experiments/occupancy_knobs.patch).
 constexpr int kExtractBlocksPerCu = 6;
 
 template <int LC>
 size_t extract_lds_pad() {
-  static const size_t pad = [] {
-    const char* env = getenv("MAGOT_EXTRACT_BLOCKS_PER_CU");
-    const int want = env ? atoi(env) : kExtractBlocksPerCu;
-    return occupancy_lds_pad(reinterpret_cast<const void*>(extract_kernel<LC>), kThreads, want);
-  }();
+  static const size_t pad = occupancy_lds_pad(reinterpret_cast<const void*>(extract_kernel<LC>),
+                                              kThreads, kExtractBlocksPerCu);
   return pad;
 }
 

@@ -847,15 +847,12 @@ void launch_orf6(const Orf6Args& a, bool genome, hipStream_t s) {
   if (a.n_tiles == 0) return;
   const uint64_t blocks = (a.n_tiles + kOpsThreads / 64 - 1) / (kOpsThreads / 64);
   if (genome) {
-    // Blocks per CU (MAGOT_ORF6_BLOCKS_PER_CU overrides; 0: no cap).  With
-    // codes staged (14.6 KB LDS, 52 VGPRs) 8 blocks fit; 7 measured best:
-    // 1.4825 / 1.4839 / 1.4799 ms per C5 step against 1.508 / 1.5071 / 1.5091
-    // uncapped and 1.4868 / 1.488 / 1.4898 at 6 (one box, alternating runs).
-    static const size_t pad = [] {
-      const char* env = getenv("MAGOT_ORF6_BLOCKS_PER_CU");
-      return occupancy_lds_pad(reinterpret_cast<const void*>(orf6_kernel<true>), kOpsThreads,
-                               env ? atoi(env) : kOrf6BlocksPerCu);
-    }();
+    // Blocks per CU.  With codes staged (14.6 KB LDS, 52 VGPRs) 8 blocks fit;
+    // 7 measured best: 1.4825 / 1.4839 / 1.4799 ms per C5 step against 1.508 /
+    // 1.5071 / 1.5091 uncapped and 1.4868 / 1.488 / 1.4898 at 6 (one box,
+    // alternating runs; the sweep override: scripts/experiments/occupancy_knobs.patch).
+    static const size_t pad = occupancy_lds_pad(reinterpret_cast<const void*>(orf6_kernel<true>),
+                                                kOpsThreads, kOrf6BlocksPerCu);
     hipLaunchKernelGGL(orf6_kernel<true>, dim3((uint32_t)blocks), dim3(kOpsThreads), pad, s, a);
   } else
     hipLaunchKernelGGL(orf6_kernel<false>, dim3((uint32_t)blocks), dim3(kOpsThreads), 0, s, a);
