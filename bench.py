@@ -611,6 +611,10 @@ def run_job(args, dist, rank, local, world):
     kernel_b2b = timer.time_b2b(n_b2b)
     kernel_iso = timer.time(10)
     kernel_ms_max = allreduce_max(dist, kernel_ms)
+    # per-rank figures of a shared job (where a scaling loss sits: the slowest
+    # rank's kernel, or the host's time around it)
+    kernel_ms_ranks = all_values(dist, kernel_ms) if dist is not None else None
+    elapsed_ranks = all_values(dist, elapsed) if dist is not None else None
     boxrec = None
     if record_box:
         boxrec = box_state(local, smi0, smi_snapshot(local), probe0, memory_probe())
@@ -709,6 +713,9 @@ def run_job(args, dist, rank, local, world):
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,
                          'kernel': kernel_name, 'kernel_ms': kernel_ms_max,
+                         'kernel_ms_per_rank': kernel_ms_ranks,
+                         'step_ms_per_rank': [e / args.steps * 1e3 for e in elapsed_ranks]
+                         if elapsed_ranks else None,
                          'kernel_ms_source': 'HIP events on the kernel\'s stream around the K '
                                              'timed launches, / K (max over ranks)',
                          'kernel_ms_b2b': kernel_b2b,

@@ -80,8 +80,11 @@ def test_bench_spawns_eight_ranks_strong():
     assert d['parity'].startswith('bit-exact'), d['parity']
     g = d['outputs_gather']
     assert g['parity'].startswith('bit-exact') and 'global record order' in g['parity'], g
-    assert d['genome_broadcast_bytes'] < 0.6 * d['genome_arena_bytes']
+    assert d['genome_broadcast_bytes'] < 0.35 * d['genome_arena_bytes']
     assert d['host']['peak_rss_gib_max_rank'] > 0
+    assert len(d['host']['peak_rss_gib_per_rank']) == 8
+    assert len(d['roofline']['kernel_ms_per_rank']) == 8
+    assert max(d['roofline']['kernel_ms_per_rank']) == d['roofline']['kernel_ms']
 
 
 @pytest.mark.parametrize('tensors', ['cpu', 'cuda'])

@@ -276,6 +276,20 @@ def test_image_round_trip_edge_genomes(shape):
     _assert_image_round_trip(contigs)
 
 
+def test_image_round_trip_fasta_loaded():
+    """A genome read and packed from FASTA text (magot_genome_load_fasta) replicates
+    through its image like one packed from contigs."""
+    w = synth.make('small', seed=4, genome_bases=300_000, n_tx=10, iupac_rate=1e-3)
+    fg = engine.FastaGenome.load(w.fasta_text(width=61).encode('latin-1'))
+    rep, n = _image_replica(fg)
+    try:
+        assert rep.export() == fg.export()
+        assert np.array_equal(_defined(fg, _arena(fg)), _defined(rep, _arena(rep)))
+    finally:
+        rep.close()
+        fg.close()
+
+
 def test_image_replica_extracts_the_same_bytes():
     w = synth.make('small', seed=12, genome_bases=2_000_000, n_tx=800, iupac_rate=1e-3)
     g = engine.DeviceGenome(w.contigs())
