@@ -70,6 +70,22 @@ class DeviceGenome(object):
         self._keepalive = None
         self._stats()
 
+    def _check_contigs(self):
+        """The caller's contig lengths against the genome's own table (a
+        replica built from a meta blob of another genome is refused)."""
+        n = ctypes.c_uint32()
+        nl = ctypes.c_uint64()
+        L = _lib.lib()
+        check(L.magot_genome_contigs(self.handle, ctypes.byref(n), None, None, 0,
+                                     ctypes.byref(nl)), 'magot_genome_contigs')
+        lens = np.zeros(max(n.value, 1), dtype=np.uint64)
+        check(L.magot_genome_contigs(self.handle, ctypes.byref(n), ptr(lens), None, 0,
+                                     ctypes.byref(nl)), 'magot_genome_contigs')
+        if n.value != len(self.names) or not np.array_equal(lens[:n.value], self.lengths):
+            self.close()
+            raise MagotError('genome replica: %d contigs in the meta blob, %d names / lengths '
+                             'given, or their lengths differ' % (n.value, len(self.names)))
+
     def _stats(self):
         tb, nr, db = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         check(_lib.lib().magot_genome_stats(self.handle, ctypes.byref(tb), ctypes.byref(nr),
@@ -135,6 +151,7 @@ class DeviceGenome(object):
                                                   ctypes.c_void_p(wire_dev_ptr), int(wire_bytes),
                                                   ctypes.byref(h)), 'magot_genome_wire_import')
         self.handle = h
+        self._check_contigs()
         self._stats()
         return self
 
@@ -161,6 +178,7 @@ class DeviceGenome(object):
         check(fn(self.ctx.handle, ptr(m), len(m), ctypes.c_void_p(arena_dev_ptr), ctypes.byref(h)),
               'magot_genome_attach')
         self.handle = h
+        self._check_contigs()
         self._stats()
         return self
 

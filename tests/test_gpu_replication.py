@@ -321,6 +321,9 @@ def test_image_refused_for_another_genome():
             engine.DeviceGenome.from_wire(meta_b, buf.data_ptr(), n, b.names, b.lengths)
         with pytest.raises(engine.MagotError):   # too small a buffer for the export
             a.wire_export(buf.data_ptr(), n - 1)
+        meta_a, _ = a.export()
+        with pytest.raises(engine.MagotError):   # the caller's contig table disagrees
+            engine.DeviceGenome.from_wire(meta_a, buf.data_ptr(), n, ['a', 'b'], [10000, 5])
     finally:
         a.close()
         b.close()
