@@ -509,7 +509,7 @@ def run_job(args, dist, rank, local, world):
         tx_bases = np.add.reduceat(w.ex_len, first[:-1])
         sh, load, _ = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), k,
                                           tx_start=w.ex_start[first[:-1]])
-        mine = sh[r]
+        mine = shard.genome_order(sh[r], w.tx_contig, w.ex_start[first[:-1]])
         rehearse = {'ranks': k, 'rank': r, 'load_imbalance': shard.imbalance(load)}
     if multi:
         first = np.zeros(w.n_tx + 1, dtype=np.int64)
@@ -517,6 +517,11 @@ def run_job(args, dist, rank, local, world):
         tx_bases = np.add.reduceat(w.ex_len, first[:-1]) if w.n_tx else np.zeros(0)
         shards, load, spans = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len),
                                                   world, tx_start=w.ex_start[first[:-1]])
+        # every rank extracts its shard in genome order: its outputs are gathered
+        # and put back into global record order anyway (reassembly), so the order
+        # inside a rank's buffer is free, and neighbouring records then share
+        # genome lines (C4 shares 7.5-9 % faster, profiles/r05/shard_order/)
+        shards = [shard.genome_order(sh, w.tx_contig, w.ex_start[first[:-1]]) for sh in shards]
         mine = shards[rank]
         imb = shard.imbalance(load)
         log('%d records over %d ranks: load imbalance %.4f%%, %d contig(s) split'
@@ -709,6 +714,10 @@ def run_job(args, dist, rank, local, world):
                        'exons_rank0': int(plan.n_exons), 'transcripts_rank0': int(plan.n_tx),
                        'parallelism': 'contig-sharded x%d (%s)' % (world,
                                                                   'strong' if strong else 'weak'),
+                       'shard_record_order': ('genome: each rank extracts its shard in '
+                                              'coordinate order; the gather\'s reassembly '
+                                              'restores global record order') if multi
+                       else None,
                        'backend': dist.get_backend() if dist is not None else None},
             'roofline': {'bound': 'hbm', 'achieved': achieved, 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS, 'traffic': traffic,

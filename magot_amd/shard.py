@@ -83,6 +83,20 @@ def record_shards(tx_contig, tx_bases, n_contigs, n_ranks, tx_start=None):
     return shards, load, spans
 
 
+def genome_order(records, tx_contig, tx_start):
+    """``records`` (global ids) sorted by (contig, first exon start): the order a
+    rank of a shared job extracts its shard in.  Its outputs land in that order
+    in the rank's buffer; the gather's reassembly puts every record back at its
+    global place (``reassembly_tables`` follows the order given), so the job's
+    output is unchanged.  Neighbouring records then share genome lines in the
+    caches: C3 in coordinate order reads 0.53 instead of 0.88 GB per launch."""
+    records = np.asarray(records, dtype=np.int64)
+    tx_contig = np.asarray(tx_contig, dtype=np.int64)
+    tx_start = np.asarray(tx_start, dtype=np.int64)
+    o = np.lexsort((records, tx_start[records], tx_contig[records]))
+    return records[o]
+
+
 def imbalance(load):
     """max / mean - 1 of per-rank loads."""
     load = np.asarray(load, dtype=np.float64)

@@ -28,6 +28,9 @@ def main():
     ap.add_argument('--rounds', type=int, default=5)
     ap.add_argument('--launches', type=int, default=200)
     ap.add_argument('--config', default='C3')
+    ap.add_argument('--order', default='gff', choices=['gff', 'genome'],
+                    help='record order inside each shard: GFF order, or genome order '
+                         '(shard.genome_order; the full job stays in GFF order)')
     a = ap.parse_args()
     from magot_amd import _lib, engine, shard, synth
     t0 = time.perf_counter()
@@ -56,6 +59,8 @@ def main():
                                               tx_start=w.ex_start[first[:-1]])
         loads[n] = load.tolist()
         for r, sh in enumerate(shards):
+            if a.order == 'genome':
+                sh = shard.genome_order(sh, w.tx_contig, w.ex_start[first[:-1]])
             plans['%d:%d' % (n, r)] = make_plan(w.plan_tables(tx_subset=sh))
     plans['one_record'] = make_plan(w.plan_tables(tx_subset=np.array([0])))
     sys.stderr.write('planned %d plans in %.1fs\n' % (len(plans), time.perf_counter() - t0))
@@ -69,7 +74,8 @@ def main():
                          % (rnd, times['full'][-1], times['2:0'][-1], times['4:0'][-1],
                             times['8:0'][-1]))
     info = ctx.info()
-    res = {'config': a.config, 'rounds': a.rounds, 'launches_per_timing': a.launches,
+    res = {'config': a.config, 'order': a.order, 'rounds': a.rounds,
+           'launches_per_timing': a.launches,
            'device': info,
            'kernel': 'orf6_kernel' if c5 else 'extract_kernel',
            'plans': {k: {'ms': v,

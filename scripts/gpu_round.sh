@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
 # stages: tests slow bench driver c2 c5 multi multi5 rehearse kt kt5 kt2 pmc traffic e2e smoke
-#         dist dist5 fetchcal gloo8c3 gloo8c5 c4shares c5shares launchcost c2order pytest:<file>
+#         dist dist5 fetchcal gloo8c3 gloo8c5 c4shares c4sharesg c5shares launchcost c2order pytest:<file>
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
 bash scripts/box_info.sh $OUT/box_before
@@ -56,6 +56,10 @@ done
 if has c4shares; then
   timeout -k 10 600 python scripts/c4_shares.py > $OUT/c4_shares.json 2> $OUT/c4_shares.err || { tail -20 $OUT/c4_shares.err; exit 1; }
   tail -8 $OUT/c4_shares.err
+fi
+if has c4sharesg; then
+  timeout -k 10 600 python scripts/c4_shares.py --order genome > $OUT/c4_shares_genome.json 2> $OUT/c4_shares_genome.err || { tail -20 $OUT/c4_shares_genome.err; exit 1; }
+  tail -8 $OUT/c4_shares_genome.err
 fi
 if has c5shares; then
   timeout -k 10 900 python scripts/c4_shares.py --config C5 --launches 50 > $OUT/c5_shares.json 2> $OUT/c5_shares.err || { tail -20 $OUT/c5_shares.err; exit 1; }

@@ -224,6 +224,36 @@ def test_reassemble_split_contig_global_order():
         assert np.array_equal(got, full) and np.array_equal(goff, foff)
 
 
+def test_genome_ordered_shards_reassemble_to_global_order():
+    """Ranks extract their shards in genome order (shard.genome_order); the
+    reassembly, which follows the order each rank's records were given in,
+    still yields the single-job output in global record order."""
+    from magot_amd import shard, synth
+    from oracle import cds_oracle
+    w = synth.make('small', seed=13, genome_bases=300_000, n_tx=300)
+    first = np.zeros(w.n_tx + 1, dtype=np.int64)
+    np.cumsum(w.ex_count, out=first[1:])
+    tx_bases = np.add.reduceat(w.ex_len, first[:-1])
+    tx_start = w.ex_start[first[:-1]]
+    shards, _, _ = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), 3,
+                                       tx_start=tx_start)
+    ordered = [shard.genome_order(sh, w.tx_contig, tx_start) for sh in shards]
+    for sh, od in zip(shards, ordered):
+        assert np.array_equal(np.sort(od), sh)                 # the same records
+        key = w.tx_contig[od] * 10**9 + tx_start[od]
+        assert np.all(np.diff(key) >= 0)                       # in genome order
+    assert any(not np.array_equal(a, b) for a, b in zip(shards, ordered))
+    for protein in (False, True):
+        full, foff, _ = cds_oracle.extract_workload(w, protein)
+        parts, offs = [], []
+        for od in ordered:
+            out, off, st = cds_oracle.extract_workload(w, protein, tx_subset=od)
+            parts.append(out)
+            offs.append(off)
+        got, goff = shard.reassemble(ordered, parts, offs)
+        assert np.array_equal(got, full) and np.array_equal(goff, foff)
+
+
 def test_reassemble_round_trip():
     from magot_amd import shard
     rng = np.random.default_rng(7)
