@@ -549,6 +549,13 @@ def run_job(args, dist, rank, local, world):
         outputs = engine.OUT_NUC
     else:
         outputs = engine.OUT_NUC | (engine.OUT_PEP if w.outputs == 'nuc+pep' else 0)
+        if args.plan_layout == 'genome' and not multi:
+            # records laid out in genome order in HBM (MAGOT_OUT_GENOME_ORDER):
+            # neighbouring loci run in neighbouring tiles and share genome lines
+            # (C3 kernel -4.7 %, C2 -3.0 %, profiles/r05/plan_order/); fetch,
+            # copy_outputs and the FASTA text assembly still deliver record order;
+            # a shared job's shards are already listed in genome order
+            outputs |= engine.OUT_GENOME_ORDER
     t0 = time.perf_counter()
     plan = engine.ExtractionPlan(dev, ex, tx, outputs)
     o6 = engine.Orf6Plan(plan) if c5 else None
@@ -714,6 +721,9 @@ def run_job(args, dist, rank, local, world):
                        'exons_rank0': int(plan.n_exons), 'transcripts_rank0': int(plan.n_tx),
                        'parallelism': 'contig-sharded x%d (%s)' % (world,
                                                                   'strong' if strong else 'weak'),
+                       'plan_layout': None if c5 else (
+                           'record (shard tables listed in genome order)' if multi
+                           else args.plan_layout),
                        'shard_record_order': ('genome: each rank extracts its shard in '
                                               'coordinate order; the gather\'s reassembly '
                                               'restores global record order') if multi
@@ -788,7 +798,7 @@ def gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx):
         items.append(('six-frame residues', o6.total, o6.copy_outputs,
                       shard.six_frame_blocks(soff, slen)))
     else:
-        _, noff, _, poff = plan.fetch()
+        noff, poff = plan.fetch_to(None, None)  # the offset tables only
         items.append(('nucleotides', plan.nuc_bytes,
                       lambda a: plan.copy_outputs(a, None), shard.places(noff)))
         if plan.outputs & engine.OUT_PEP:
@@ -865,6 +875,9 @@ def main(argv=None):
     ap.add_argument('--order', default='random', choices=['random', 'sorted'],
                     help='record order of the synthetic GFF: random within each contig '
                          '(default, SURVEY 8(d)) or coordinate-sorted (diagnostic)')
+    ap.add_argument('--plan-layout', default='genome', choices=['genome', 'record'],
+                    help='extraction plans: records laid out in HBM in genome order (default; '
+                         'delivery returns record order) or in record order')
     ap.add_argument('--no-verify', action='store_true', help='skip the oracle byte check')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-box-state', action='store_true',

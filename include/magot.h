@@ -46,6 +46,14 @@ enum magot_status {
 /* Output selection for a plan (magot_plan_create.outputs). */
 #define MAGOT_OUT_NUC 1u   /* spliced CDS nucleotides  (seq_type="nucleotide") */
 #define MAGOT_OUT_PEP 2u   /* frame-0 translation      (seq_type="protein")    */
+/* Layout flag: lay the records out in the device buffers in genome order (by
+ * the coordinate of each record's first non-empty interval) instead of record
+ * order.  Neighbouring loci then run in neighbouring tiles and share genome
+ * lines.  magot_plan_fetch, magot_plan_copy_outputs and magot_fasta_text_*
+ * still deliver record order (a device segment copy puts the records back);
+ * magot_plan_layout gives each record's place in the device buffers.  Such a
+ * plan has no six-frame plan (magot_plan_orf6 refuses it). */
+#define MAGOT_OUT_GENOME_ORDER 4u
 
 /*
  * One interval of one record, already in OUTPUT order.
@@ -284,11 +292,22 @@ int magot_plan_time(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms);
 int magot_plan_time_b2b(magot_ctx* ctx, magot_plan* p, int iters, double* avg_ms);
 
 /* D2D copy of a plan's outputs (nuc_bytes / pep_bytes) into caller device
- * memory, e.g. the buffers an output gather sends. */
+ * memory, e.g. the buffers an output gather sends, in record order (a
+ * genome-ordered plan's records are put back by a segment copy: its
+ * destinations must then be 16-byte aligned, else MAGOT_ERR_ARG). */
 int magot_plan_copy_outputs(magot_ctx* ctx, magot_plan* p, void* nuc_dst_dev, void* pep_dst_dev);
 
-/* Device-resident output pointers of a plan (for on-device consumers/tests). */
+/* Device-resident output pointers of a plan (for on-device consumers/tests).
+ * The buffers hold the records in the plan's layout order: record t starts at
+ * magot_plan_layout's nuc_start[t] / pep_start[t] and is as long as its
+ * prefix offsets (magot_plan_fetch) say. */
 int magot_plan_device_outputs(magot_plan* p, void** nuc_dev, void** pep_dev);
+
+/* Each record's start in the plan's device buffers (n_tx entries each; either
+ * pointer may be NULL): the prefix offsets for a record-order plan, the
+ * genome-order places for a MAGOT_OUT_GENOME_ORDER one.  No reference
+ * counterpart (device layout). */
+int magot_plan_layout(const magot_plan* p, uint64_t* nuc_start, uint64_t* pep_start);
 
 /* Algorithmic byte count per execute of a plan (the roofline numerator):
  * ceil(B/4) + B*[nuc] + P*[pep] + 16*E + 32*T. */

@@ -17,6 +17,7 @@ LIB_PATH = os.environ.get('MAGOT_LIB') or os.path.join(HERE, 'libmagot.so')
 
 OUT_NUC = 1
 OUT_PEP = 2
+OUT_GENOME_ORDER = 4  # layout flag: records in genome order in the device buffers
 
 EXON_DTYPE = np.dtype([('start_rc', '<u8'), ('contig', '<u4'), ('len', '<u4')])
 TX_DTYPE = np.dtype([('exon_begin', '<u8'), ('n_exons', '<u4'), ('flags', '<u4')])
@@ -29,6 +30,7 @@ EXPORTS = (
     'magot_genome_load', 'magot_genome_stats', 'magot_genome_destroy',
     'magot_plan_create', 'magot_plan_destroy', 'magot_plan_execute', 'magot_plan_fetch',
     'magot_run', 'magot_plan_time', 'magot_plan_time_b2b', 'magot_plan_device_outputs',
+    'magot_plan_layout',
     'magot_plan_algorithmic_bytes',
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
     'magot_codon_symbols', 'magot_revcomp', 'magot_translate',
@@ -93,6 +95,7 @@ def _declare(lib):
                                            ctypes.POINTER(ctypes.c_double)]),
         'magot_plan_time_b2b': (ctypes.c_int, [_vp, _vp, ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_double)]),
+        'magot_plan_layout': (ctypes.c_int, [_vp, _vp, _vp]),
         'magot_plan_device_outputs': (ctypes.c_int, [_vp, ctypes.POINTER(_vp),
                                                      ctypes.POINTER(_vp)]),
         'magot_plan_algorithmic_bytes': (ctypes.c_uint64, [_vp]),

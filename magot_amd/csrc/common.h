@@ -338,7 +338,7 @@ struct TextUnit {
 bool gffplan_units(const magot_gffplan* p, const std::string** text, std::vector<TextUnit>* units,
                    bool* protein, uint64_t* n_rec);
 size_t text_scan_bytes(uint64_t n);
-void launch_text_assembly(const TextUnit* units, uint64_t n, const uint64_t* roff,
+void launch_text_assembly(const TextUnit* units, uint64_t n, const uint64_t* rspan,
                           const uint8_t* pay, int protein, const uint8_t* text, uint64_t* len,
                           uint64_t* end, void* scan_tmp, size_t scan_bytes, uint8_t* out,
                           hipStream_t s);

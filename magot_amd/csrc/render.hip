@@ -25,33 +25,34 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kUnroll = 8;
 
-__device__ inline void unit_payload(const TextUnit& u, const uint64_t* roff, const uint8_t* pay,
+// rspan: each record's {start, end} in the payload buffer (the plan's layout)
+__device__ inline void unit_payload(const TextUnit& u, const uint64_t* rspan, const uint8_t* pay,
                                     int protein, uint64_t* a, uint64_t* len) {
   if (u.rec == kNoRecord) {
     *a = 0;
     *len = 0;
     return;
   }
-  uint64_t s = roff[u.rec];
-  const uint64_t e = roff[u.rec + 1];
+  uint64_t s = rspan[2 * (uint64_t)u.rec];
+  const uint64_t e = rspan[2 * (uint64_t)u.rec + 1];
   if (protein && e > s && pay[s] == 'X') ++s;
   *a = s;
   *len = e - s;
 }
 
 __global__ void text_len_kernel(const TextUnit* __restrict__ units, uint64_t n,
-                                const uint64_t* __restrict__ roff, const uint8_t* __restrict__ pay,
+                                const uint64_t* __restrict__ rspan, const uint8_t* __restrict__ pay,
                                 int protein, uint64_t* __restrict__ len) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const TextUnit u = units[i];
   uint64_t a, pl;
-  unit_payload(u, roff, pay, protein, &a, &pl);
+  unit_payload(u, rspan, pay, protein, &a, &pl);
   len[i] = u.text_len + pl;
 }
 
 __global__ __launch_bounds__(256) void text_copy_kernel(
-    const TextUnit* __restrict__ units, uint64_t n, const uint64_t* __restrict__ roff,
+    const TextUnit* __restrict__ units, uint64_t n, const uint64_t* __restrict__ rspan,
     const uint8_t* __restrict__ pay, int protein, const uint8_t* __restrict__ text,
     const uint64_t* __restrict__ end, uint8_t* __restrict__ out) {
   // wave index: readfirstlane takes 32 bits, so the (wave-uniform) block part
@@ -62,7 +63,7 @@ __global__ __launch_bounds__(256) void text_copy_kernel(
   const int lane = threadIdx.x % kWave;
   const TextUnit u = units[w];
   uint64_t a, pl;
-  unit_payload(u, roff, pay, protein, &a, &pl);
+  unit_payload(u, rspan, pay, protein, &a, &pl);
   const uint64_t tl = u.text_len;
   const uint64_t total = tl + pl;
   const uint8_t* t = text + u.text_off;
@@ -92,17 +93,17 @@ size_t text_scan_bytes(uint64_t n) {
   return bytes;
 }
 
-void launch_text_assembly(const TextUnit* units, uint64_t n, const uint64_t* roff,
+void launch_text_assembly(const TextUnit* units, uint64_t n, const uint64_t* rspan,
                           const uint8_t* pay, int protein, const uint8_t* text, uint64_t* len,
                           uint64_t* end, void* scan_tmp, size_t scan_bytes, uint8_t* out,
                           hipStream_t s) {
   if (!n) return;
-  text_len_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(units, n, roff, pay, protein, len);
+  text_len_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(units, n, rspan, pay, protein, len);
   (void)rocprim::inclusive_scan(scan_tmp, scan_bytes, len, end, (size_t)n,
                                 rocprim::plus<uint64_t>(), s);
   const uint64_t waves_per_block = 256 / kWave;
   text_copy_kernel<<<(unsigned)((n + waves_per_block - 1) / waves_per_block), 256, 0, s>>>(
-      units, n, roff, pay, protein, text, end, out);
+      units, n, rspan, pay, protein, text, end, out);
 }
 
 }  // namespace magot

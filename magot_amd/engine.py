@@ -8,7 +8,8 @@ import os
 import numpy as np
 
 from . import _lib
-from ._lib import EXON_DTYPE, TX_DTYPE, OUT_NUC, OUT_PEP, MagotError, check, ptr
+from ._lib import (EXON_DTYPE, TX_DTYPE, OUT_NUC, OUT_PEP, OUT_GENOME_ORDER, MagotError, check,
+                   ptr)
 
 
 def _as_bytes(s):
@@ -427,7 +428,10 @@ class ExtractionPlan(object):
     """Interval table -> device plan (magot_plan_create).
 
     ``exons``: structured array of EXON_DTYPE in output order; ``txs``:
-    structured array of TX_DTYPE tiling it.  ``outputs``: OUT_NUC | OUT_PEP.
+    structured array of TX_DTYPE tiling it.  ``outputs``: OUT_NUC | OUT_PEP,
+    optionally | OUT_GENOME_ORDER (records laid out in genome order on the
+    device; fetch / copy_outputs still return record order, ``layout()`` gives
+    each record's place in the device buffers).
     """
 
     def __init__(self, genome, exons, txs, outputs=OUT_NUC | OUT_PEP):
@@ -471,6 +475,15 @@ class ExtractionPlan(object):
     def run(self):
         self.execute()
         return self.fetch()
+
+    def layout(self):
+        """(nuc_start uint64[T], pep_start uint64[T]): each record's start in
+        the device buffers (magot_plan_layout)."""
+        ns = np.empty(self.n_tx, dtype=np.uint64)
+        ps = np.empty(self.n_tx, dtype=np.uint64)
+        check(_lib.lib().magot_plan_layout(self.handle, ptr(ns) if self.n_tx else None,
+                                           ptr(ps) if self.n_tx else None), 'magot_plan_layout')
+        return ns, ps
 
     def copy_outputs(self, nuc_dev_ptr=None, pep_dev_ptr=None):
         """D2D copy of the outputs into caller device memory (addresses)."""

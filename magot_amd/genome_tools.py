@@ -159,8 +159,12 @@ def _gff2fasta_run(genome_sequence, dev, plan, plan_gff):
         if plan is None:
             return None, seqs
     try:
+        # the device text assembly reads each record where the plan laid it
+        # out, so the extraction runs in genome order (neighbouring loci in
+        # neighbouring tiles); host renders keep record order
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
-                                   engine.OUT_PEP if plan.protein else engine.OUT_NUC)
+                                   (engine.OUT_PEP if plan.protein else engine.OUT_NUC)
+                                   | (0 if plan.n_select else engine.OUT_GENOME_ORDER))
         if plan.n_select:
             # longest=True over peptides: the render picks from the trimmed
             # lengths, on the host
@@ -376,7 +380,8 @@ def _flank_native(genome_sequence, gff, sequence_length, stream, feature_type, n
     try:
         if len(plan.txs) == 0:
             return b''
-        ex = engine.ExtractionPlan(dev, plan.exons, plan.txs, engine.OUT_NUC)
+        ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
+                                   engine.OUT_NUC | engine.OUT_GENOME_ORDER)
         text = engine.FastaText(plan, ex)
         try:
             ex.execute()

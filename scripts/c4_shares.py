@@ -30,7 +30,8 @@ def main():
     ap.add_argument('--config', default='C3')
     ap.add_argument('--order', default='gff', choices=['gff', 'genome'],
                     help='record order inside each shard: GFF order, or genome order '
-                         '(shard.genome_order; the full job stays in GFF order)')
+                         '(shard.genome_order; the full C3 job then runs as bench.py runs '
+                         'it, its records laid out in genome order)')
     a = ap.parse_args()
     from magot_amd import _lib, engine, shard, synth
     t0 = time.perf_counter()
@@ -44,15 +45,16 @@ def main():
     outputs = engine.OUT_NUC if c5 else engine.OUT_NUC | engine.OUT_PEP
     keep = []
 
-    def make_plan(tables):
+    def make_plan(tables, flags=0):
         """The timed object: the extraction plan (C3), or its six-frame plan (C5)."""
-        p = engine.ExtractionPlan(dev, *tables, outputs)
+        p = engine.ExtractionPlan(dev, *tables, outputs | flags)
         if not c5:
             return p
         keep.append(p)
         return engine.Orf6Plan(p)
 
-    plans = {'full': make_plan(w.plan_tables())}
+    full_flags = engine.OUT_GENOME_ORDER if a.order == 'genome' and not c5 else 0
+    plans = {'full': make_plan(w.plan_tables(), full_flags)}
     loads = {}
     for n in (2, 4, 8):
         shards, load, _ = shard.record_shards(w.tx_contig, tx_bases, len(w.contig_len), n,
@@ -75,6 +77,7 @@ def main():
                             times['8:0'][-1]))
     info = ctx.info()
     res = {'config': a.config, 'order': a.order, 'rounds': a.rounds,
+           'full_job_layout': 'genome' if full_flags else 'record',
            'launches_per_timing': a.launches,
            'device': info,
            'kernel': 'orf6_kernel' if c5 else 'extract_kernel',

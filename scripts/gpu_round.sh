@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 TAG=${1:-r01}; shift
 STAGES=${*:-tests slow bench kt pmc}
 # stages: tests slow bench driver c2 c5 multi multi5 rehearse kt kt5 kt2 pmc traffic e2e smoke
-#         dist dist5 fetchcal gloo8c3 gloo8c5 c4shares c4sharesg c5shares launchcost c2order pytest:<file>
+#         dist dist5 fetchcal gloo8c3 gloo8c5 c4shares c4sharesg c5shares launchcost c2order planorder pytest:<file>
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 BENCH="bench.py"
 bash scripts/box_info.sh $OUT/box_before
@@ -74,6 +74,11 @@ fi
 if has c2order; then
   timeout -k 10 300 python scripts/c2_draw_order.py > $OUT/c2_draw_order.json 2> $OUT/c2_draw_order.err || { tail -20 $OUT/c2_draw_order.err; exit 1; }
   cat $OUT/c2_draw_order.json
+fi
+if has planorder; then
+  # record- vs genome-order extraction plans, alternating rounds (scripts/plan_order_ab.py)
+  timeout -k 10 600 python scripts/plan_order_ab.py > $OUT/plan_order.json 2> $OUT/plan_order.err || { tail -20 $OUT/plan_order.err; exit 1; }
+  tail -16 $OUT/plan_order.err
 fi
 if has slow; then
   timeout -k 10 900 python -u -m pytest tests -m "gpu and slow" -q --timeout 600 --timeout-method thread > $OUT/pytest_gpu_slow.log 2>&1 || { tail -40 $OUT/pytest_gpu_slow.log; exit 1; }
