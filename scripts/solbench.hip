@@ -23,7 +23,10 @@
 //     wave (staging's shape), with loads and stores in the same or in
 //     separate waves, and with extra load instructions per round.
 // c5 now: the chain over round 4's layout and block order.
-//   usage: solbench c3 | solbench c5 [chain | now]
+// c3now: the C3 launch with its records laid out in genome order (round 5):
+//     35 line fills per tile (0.53 GB per launch, PMC), tile w's lines
+//     following tile w-1's, the same stores.
+//   usage: solbench c3 | solbench c3now | solbench c5 [chain | now]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -64,6 +67,7 @@ struct C3Args {
   uint32_t* sink;
   uint32_t win_tiles;     // reads: inside a moving window (one contig) of this many tiles (0: anywhere)
   uint64_t win_lines;     // lines per window
+  uint32_t seq;           // reads walk the planes in tile order (genome-order layout)
 };
 
 __global__ __launch_bounds__(256) void c3_replay(C3Args a) {
@@ -76,7 +80,8 @@ __global__ __launch_bounds__(256) void c3_replay(C3Args a) {
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const uint32_t l = lane + 64 * k;
-    const uint64_t line = a.win_tiles ? ((w / a.win_tiles) * a.win_lines + mix(w * 256 + l) % a.win_lines) % a.plane_lines
+    const uint64_t line = a.seq ? (w * a.lines + l) % a.plane_lines
+                          : a.win_tiles ? ((w / a.win_tiles) * a.win_lines + mix(w * 256 + l) % a.win_lines) % a.plane_lines
                                       : mix(w * 256 + l) % a.plane_lines;
     v[k] = l < a.lines ? *reinterpret_cast<const uint3*>(a.plane + line * 128 + 16 * (l & 7))
                        : make_uint3(0, 0, 0);
@@ -97,6 +102,41 @@ __global__ __launch_bounds__(256) void c3_replay(C3Args a) {
     if (16 * c < a.pep_bytes) st16(p0 + 16 * c, make_uint4(acc, c, s, (uint32_t)w), true);
   }
   if (acc == 0x12345678u) *a.sink = acc;
+}
+
+// store-only variants of C3's output stream: each wave writes `per_wave`
+// consecutive tiles (nuc then pep per tile), nt or plain 16-B stores, in
+// the launch's XCD runs of `xrun` blocks (0: hardware round-robin)
+template <bool kNt>
+__global__ __launch_bounds__(256) void c3_stores(uint8_t* nuc, uint8_t* pep, uint32_t ntiles,
+                                                 uint32_t nuc_bytes, uint32_t pep_bytes,
+                                                 uint32_t per_wave, uint32_t xrun) {
+  uint32_t vb = blockIdx.x;
+  if (xrun) {
+    // runs of xrun consecutive blocks per XCD (extract_kernel's kXcdRun order)
+    const uint32_t nb = gridDim.x, xcd = vb & 7, k = vb >> 3;
+    const uint32_t run = k / xrun, in = k % xrun;
+    const uint32_t v = (run * 8 + xcd) * xrun + in;
+    vb = v < nb ? v : vb;
+  }
+  const uint64_t w = (uint64_t)vb * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  for (uint32_t j = 0; j < per_wave; ++j) {
+    const uint64_t t = w * per_wave + j;
+    if (t >= ntiles) return;
+    uint8_t* const n0 = nuc + t * nuc_bytes;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const uint32_t c = 64 * s + lane;
+      if (16 * c < nuc_bytes) st16(n0 + 16 * c, make_uint4(c, s, (uint32_t)t, 1), kNt);
+    }
+    uint8_t* const p0 = pep + t * pep_bytes;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t c = 64 * s + lane;
+      if (16 * c < pep_bytes) st16(p0 + 16 * c, make_uint4(c, s, (uint32_t)t, 2), kNt);
+    }
+  }
 }
 
 struct C5Args {
@@ -228,7 +268,55 @@ int main(int argc, char** argv) {
              wbytes / 1e9, rbytes / 1e9, (wbytes + rbytes) / (ms * 1e6));
     }
   };
-  if (!strcmp(mode, "c3")) {
+  if (!strcmp(mode, "c3now")) {
+    // profiles/r05/final: 118,356 tiles, reads 0.536 GB (35 lines per tile)
+    const uint32_t ntiles = 118356, nuc = 5072, pep = 1696;
+    const uint64_t plane = 2ull << 30;
+    uint8_t *pl, *o1, *o2;
+    CK(hipMalloc(&pl, plane));
+    CK(hipMalloc(&o1, (uint64_t)ntiles * nuc));
+    CK(hipMalloc(&o2, (uint64_t)ntiles * pep));
+    CK(hipMemset(pl, 1, plane));
+    const size_t pad = lds_pad(reinterpret_cast<const void*>(c3_replay), 6);
+    const int grid = (int)((ntiles + 3) / 4);
+    for (uint32_t seq : {1u, 0u}) {
+      for (uint32_t lines : {35u, 0u}) {
+        C3Args a{pl, plane / 128, o1, o2, ntiles, lines, nuc, pep, sink, 0u, 0u, seq};
+        char nm[96];
+        snprintf(nm, sizeof nm, "c3now: %u fills per tile, %s", lines,
+                 seq ? "in tile order" : "scattered");
+        timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, a); }, nm,
+               (double)ntiles * (nuc + pep), (double)ntiles * lines * 128);
+      }
+    }
+    for (uint32_t per : {1u, 2u, 4u, 8u})
+      for (uint32_t xrun : {0u, 16u})
+        for (int nt = 1; nt >= 0; --nt) {
+          const int g = (int)((ntiles + 4 * per - 1) / (4 * per));
+          char nm[96];
+          snprintf(nm, sizeof nm, "stores: %u tiles/wave, xrun %u, %s", per, xrun,
+                   nt ? "nt" : "plain");
+          if (nt)
+            timeit([&] { hipLaunchKernelGGL(c3_stores<true>, g, 256, pad, 0, o1, o2, ntiles,
+                                            nuc, pep, per, xrun); },
+                   nm, (double)ntiles * (nuc + pep), 0.0);
+          else
+            timeit([&] { hipLaunchKernelGGL(c3_stores<false>, g, 256, pad, 0, o1, o2, ntiles,
+                                            nuc, pep, per, xrun); },
+                   nm, (double)ntiles * (nuc + pep), 0.0);
+        }
+    {
+      // one flat grid-stride fill of the same bytes (what a library memset does)
+      CK(hipMemsetAsync(o1, 7, (uint64_t)ntiles * nuc));
+      timeit([&] {
+        (void)hipMemsetAsync(o1, 7, (uint64_t)ntiles * nuc);
+        (void)hipMemsetAsync(o2, 7, (uint64_t)ntiles * pep);
+      }, "hipMemset of the same bytes", (double)ntiles * (nuc + pep), 0.0);
+    }
+    C3Args c{pl, plane / 128, o1, o2, ntiles, 35u, 0u, 0u, sink, 0u, 0u, 1u};
+    timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, c); },
+           "c3now: 35 fills in tile order, no stores", 0.0, (double)ntiles * 35 * 128);
+  } else if (!strcmp(mode, "c3")) {
     // C3 (profiles/r03_close2): 118,356 tiles; 600.3 MB nucleotides and
     // 199.9 MB residues; PMC line fills 0.86 GB per launch (~57 per tile)
     const uint32_t ntiles = 118356, nuc = 5072, pep = 1696;
@@ -241,28 +329,28 @@ int main(int argc, char** argv) {
     const size_t pad = lds_pad(reinterpret_cast<const void*>(c3_replay), 6);
     const int grid = (int)((ntiles + 3) / 4);
     for (uint32_t lines : {0u, 57u, 96u}) {
-      C3Args a{pl, plane / 128, o1, o2, ntiles, lines, nuc, pep, sink, 0u, 0u};
+      C3Args a{pl, plane / 128, o1, o2, ntiles, lines, nuc, pep, sink, 0u, 0u, 0u};
       char nm[96];
       snprintf(nm, sizeof nm, "c3 replay: %u line fills per tile", lines);
       timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, a); }, nm,
              (double)ntiles * (nuc + pep), (double)ntiles * lines * 128);
     }
-    C3Args a{pl, plane / 128, o1, o2, ntiles, 57u, nuc, 0u, sink, 0u, 0u};
+    C3Args a{pl, plane / 128, o1, o2, ntiles, 57u, nuc, 0u, sink, 0u, 0u, 0u};
     timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, a); },
            "c3 replay: nucleotide stores only + 57 fills", (double)ntiles * nuc,
            (double)ntiles * 57 * 128);
-    C3Args c{pl, plane / 128, o1, o2, ntiles, 57u, 0u, 0u, sink, 0u, 0u};
+    C3Args c{pl, plane / 128, o1, o2, ntiles, 57u, 0u, 0u, sink, 0u, 0u, 0u};
     timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, c); },
            "c3 replay: 57 fills, no stores", 0.0, (double)ntiles * 57 * 128);
     // C3's records are contig-major (random within a contig): the tiles of
     // one contig (64 contigs: ~1850 tiles) read inside its stretch of the two
     // planes (~2 x 7.8 MB)
     const uint64_t wl = (2ull * 7800000) / 128;
-    C3Args d{pl, plane / 128, o1, o2, ntiles, 57u, nuc, pep, sink, 1850u, wl};
+    C3Args d{pl, plane / 128, o1, o2, ntiles, 57u, nuc, pep, sink, 1850u, wl, 0u};
     timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, d); },
            "c3 replay: 57 fills within a contig's planes", (double)ntiles * (nuc + pep),
            (double)ntiles * 57 * 128);
-    C3Args e{pl, plane / 128, o1, o2, ntiles, 57u, 0u, 0u, sink, 1850u, wl};
+    C3Args e{pl, plane / 128, o1, o2, ntiles, 57u, 0u, 0u, sink, 1850u, wl, 0u};
     timeit([&] { hipLaunchKernelGGL(c3_replay, grid, 256, pad, 0, e); },
            "c3 replay: 57 fills within a contig, no stores", 0.0, (double)ntiles * 57 * 128);
   } else {
