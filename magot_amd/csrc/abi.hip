@@ -392,6 +392,24 @@ struct DevBuf {
   }
 };
 
+// Record indices in ascending key order, ties in index order: an LSD radix
+// sort in 11-bit digits, as many passes as the largest key needs.
+void radix_order(const std::vector<uint64_t>& key, std::vector<uint32_t>* out) {
+  const uint64_t n = key.size();
+  uint64_t top = 0;
+  for (uint64_t k : key) top = std::max(top, k);
+  std::vector<uint32_t> a(n), b(n);
+  for (uint64_t i = 0; i < n; ++i) a[i] = (uint32_t)i;
+  for (int shift = 0; shift < 64 && (top >> shift); shift += 11) {
+    std::vector<uint64_t> cnt(2049, 0);
+    for (uint64_t i = 0; i < n; ++i) ++cnt[((key[a[i]] >> shift) & 2047) + 1];
+    for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
+    for (uint64_t i = 0; i < n; ++i) b[cnt[(key[a[i]] >> shift) & 2047]++] = a[i];
+    a.swap(b);
+  }
+  out->swap(a);
+}
+
 // A genome-ordered plan's output (nucleotides, or residues) put back into
 // record order at dst (16-byte aligned device memory): one segment copy per
 // record from its layout place to its record-order offset, on the context stream.
@@ -971,36 +989,17 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     return MAGOT_ERR_ARG;
   }
   const uint64_t n_contigs = g->contig_base.size();
-  // Layout order of the records: record order, or (MAGOT_OUT_GENOME_ORDER) by
-  // the genome coordinate of each record's first non-empty interval, so that
-  // records sharing genome lines run in neighbouring tiles (C3: fills 0.88 ->
-  // 0.53 GB per launch); the output places come back through magot_plan_layout
-  // and fetch / copy_outputs restore record order.
-  std::vector<uint64_t> order(T);
-  for (uint64_t t = 0; t < T; ++t) order[t] = t;
-  if (by_genome) {
-    std::vector<uint64_t> key(T, ~0ull);
-    for (uint64_t t = 0; t < T; ++t) {
-      const uint64_t e0 = txs[t].exon_begin, e1 = e0 + txs[t].n_exons;
-      for (uint64_t e = e0; e < e1; ++e)
-        if (exons[e].len && exons[e].contig < n_contigs) {
-          key[t] = g->contig_base[exons[e].contig] + (exons[e].start_rc & ~kRcBit);
-          break;
-        }
-    }
-    std::stable_sort(order.begin(), order.end(),
-                     [&](uint64_t a, uint64_t b) { return key[a] < key[b]; });
-  }
-  // Compacted interval table in layout order: zero-length intervals add no output.
-  std::vector<uint64_t> ex_g, ex_out;
-  ex_g.reserve(E);
-  ex_out.reserve(E + 1);
-  std::vector<uint64_t> lay_nuc(T), lay_pep(T);  // each record's place (record order)
-  uint64_t acc = 0, P = 0;
-  for (uint64_t k = 0; k < T; ++k) {
-    const uint64_t t = order[k];
-    lay_nuc[t] = acc;
-    lay_pep[t] = P;
+  // Pass 1, record order: every interval validated, flagged and compacted
+  // (zero-length intervals add no output) into words w_g / lengths w_len;
+  // record t's compacted intervals are [rec_ex[t], rec_ex[t+1]).
+  std::vector<uint64_t> w_g;
+  std::vector<uint32_t> w_len;
+  w_g.reserve(E);
+  w_len.reserve(E);
+  std::vector<uint64_t> rec_ex(T + 1), rec_len(T);
+  for (uint64_t t = 0; t < T; ++t) {
+    rec_ex[t] = w_g.size();
+    uint64_t len = 0;
     const uint64_t e0 = txs[t].exon_begin, e1 = e0 + txs[t].n_exons;
     for (uint64_t e = e0; e < e1; ++e) {
       const magot_exon& x = exons[e];
@@ -1024,36 +1023,62 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
             break;
           }
       }
-      ex_g.push_back(gs | (x.start_rc & kRcBit) | exc);
-      ex_out.push_back(acc);
-      acc += x.len;
+      w_g.push_back(gs | (x.start_rc & kRcBit) | exc);
+      w_len.push_back(x.len);
+      len += x.len;
     }
-    P += (acc - lay_nuc[t]) / 3;
+    rec_len[t] = len;
+  }
+  rec_ex[T] = w_g.size();
+  const uint64_t Ec = w_g.size();
+  // Layout order of the records: record order, or (MAGOT_OUT_GENOME_ORDER) by
+  // the genome position of each record's first non-empty interval (records
+  // without output last), so that records sharing genome lines run in
+  // neighbouring tiles (C3: fills 0.89 -> 0.54 GB per launch); the places come
+  // back through magot_plan_layout, and fetch / copy_outputs restore record order.
+  std::vector<uint32_t> order;
+  if (by_genome) {
+    std::vector<uint64_t> key(T);
+    for (uint64_t t = 0; t < T; ++t)
+      key[t] = rec_ex[t] < rec_ex[t + 1] ? w_g[rec_ex[t]] & ~kExFlagBits : g->span;
+    radix_order(key, &order);
+  }
+  // Pass 2, layout order: the interval table with its output offsets, and
+  // each record's place (lay_*, indexed by record)
+  std::vector<uint64_t> ex_g, ex_out;
+  ex_out.reserve(Ec + 1);
+  std::vector<uint64_t> lay_nuc(T), lay_pep(T);
+  uint64_t acc = 0, P = 0;
+  if (!by_genome) ex_g.swap(w_g);
+  else ex_g.reserve(Ec);
+  for (uint64_t k = 0; k < T; ++k) {
+    const uint64_t t = by_genome ? order[k] : k;
+    lay_nuc[t] = acc;
+    lay_pep[t] = P;
+    for (uint64_t i = rec_ex[t]; i < rec_ex[t + 1]; ++i) {
+      if (by_genome) ex_g.push_back(w_g[i]);
+      ex_out.push_back(acc);
+      acc += w_len[i];
+    }
+    P += rec_len[t] / 3;
   }
   const uint64_t B = acc;
-  const uint64_t Ec = ex_g.size();
   ex_out.push_back(B);
   // Compacted record table in layout order: records with at least one codon.
   std::vector<uint64_t> tn, tp;
   for (uint64_t k = 0; k < T; ++k) {
-    const uint64_t t = order[k];
-    const uint64_t nlen = (k + 1 < T ? lay_nuc[order[k + 1]] : B) - lay_nuc[t];
-    if (nlen >= 3) {
+    const uint64_t t = by_genome ? order[k] : k;
+    if (rec_len[t] >= 3) {
       tn.push_back(lay_nuc[t]);
       tp.push_back(lay_pep[t]);
     }
   }
   // record-order prefix offsets (what fetch returns)
   std::vector<uint64_t> nuc_off(T + 1), pep_off(T + 1);
-  {
-    std::vector<uint64_t> nlen(T);
-    for (uint64_t k = 0; k < T; ++k)
-      nlen[order[k]] = (k + 1 < T ? lay_nuc[order[k + 1]] : B) - lay_nuc[order[k]];
-    nuc_off[0] = pep_off[0] = 0;
-    for (uint64_t t = 0; t < T; ++t) {
-      nuc_off[t + 1] = nuc_off[t] + nlen[t];
-      pep_off[t + 1] = pep_off[t] + nlen[t] / 3;
-    }
+  nuc_off[0] = pep_off[0] = 0;
+  for (uint64_t t = 0; t < T; ++t) {
+    nuc_off[t + 1] = nuc_off[t] + rec_len[t];
+    pep_off[t + 1] = pep_off[t] + rec_len[t] / 3;
   }
   const uint64_t Tc = tn.size();
   tn.push_back(B);

@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--configs', default='C3,C2')
     ap.add_argument('--rounds', type=int, default=7)
+    ap.add_argument('--plan-only', action='store_true', help='only the plan_create timing')
     ap.add_argument('--launches', type=int, default=200)
     a = ap.parse_args()
     import torch  # the HIP runtime torch loads first
@@ -35,9 +36,24 @@ def main():
         dev = engine.DeviceGenome(w.contig_views(), ctx=ctx)
         ex, tx = w.plan_tables()
         outputs = engine.OUT_NUC | (engine.OUT_PEP if w.outputs == 'nuc+pep' else 0)
+        sys.stderr.write('%s: generated and packed in %.1fs\n' % (cfg, time.perf_counter() - t0))
+        # host cost of magot_plan_create, 3 alternating builds of each layout
+        plan_s = {'record': [], 'genome': []}
+        for _ in range(3):
+            for k, fl in (('record', 0), ('genome', engine.OUT_GENOME_ORDER)):
+                t1 = time.perf_counter()
+                engine.ExtractionPlan(dev, ex, tx, outputs | fl).close()
+                plan_s[k].append(time.perf_counter() - t1)
+        sys.stderr.write('%s: plan_create s %s\n' % (cfg, {k: [round(x, 4) for x in v]
+                                                          for k, v in plan_s.items()}))
         plans = {'record': engine.ExtractionPlan(dev, ex, tx, outputs),
                  'genome': engine.ExtractionPlan(dev, ex, tx, outputs | engine.OUT_GENOME_ORDER)}
-        sys.stderr.write('%s: planned in %.1fs\n' % (cfg, time.perf_counter() - t0))
+        if a.plan_only:
+            res['configs'][cfg] = {'plan_create_s': plan_s}
+            for p in plans.values():
+                p.close()
+            dev.close()
+            continue
         for p in plans.values():
             p.time_b2b(20)
         times = {k: [] for k in plans}
@@ -62,7 +78,7 @@ def main():
             'records': int(w.n_tx), 'nuc_bytes': int(B), 'pep_bytes': int(P),
             'kernel_ms': times, 'median_ms': med,
             'genome_over_record': med['genome'] / med['record'],
-            'copy_outputs_ms': deliver,
+            'copy_outputs_ms': deliver, 'plan_create_s': plan_s,
             'algorithmic_bytes': plans['record'].algorithmic_bytes}
         for p in plans.values():
             p.close()
