@@ -19,7 +19,7 @@ ARCH = os.environ.get('MAGOT_OFFLOAD_ARCH', 'gfx950')
 
 SOURCES = ['abi.hip', 'extract.hip', 'seqops.hip', 'pack.cpp', 'gffplan.cpp', 'fasta.cpp',
            'render.hip', 'devpack.hip', 'wire.hip']
-HEADERS = ['common.h', os.path.join('..', '..', 'include', 'magot.h')]
+HEADERS = ['common.h', 'wavecopy.h', os.path.join('..', '..', 'include', 'magot.h')]
 
 CXXFLAGS = ['-O3', '-std=c++17', '-fPIC', '-Wall', '-Wno-unused-function',
             '--offload-arch=' + ARCH, '-I' + os.path.join(ROOT, 'include')]

@@ -2108,6 +2108,7 @@ struct magot_fasta_text {
   const uint64_t* roff = nullptr;
   const uint8_t* text = nullptr;
   uint64_t* len = nullptr;
+  uint64_t* psrc = nullptr;  // each unit's payload start in the plan's buffer
   uint64_t* end = nullptr;
   void* scan_tmp = nullptr;
   size_t scan_bytes = 0;
@@ -2116,7 +2117,7 @@ struct magot_fasta_text {
   int protein = 0;
   void launch(hipStream_t s) const {
     launch_text_assembly(units, n_units, roff, protein ? plan->args.pep : plan->args.nuc,
-                         protein, text, len, end, scan_tmp, scan_bytes, out, s);
+                         protein, text, len, psrc, end, scan_tmp, scan_bytes, out, s);
   }
 };
 
@@ -2163,6 +2164,7 @@ int magot_fasta_text_create(magot_ctx* ctx, const magot_gffplan* gp, const magot
   const uint64_t o_roff = cv.take<uint64_t>(span.size());
   const uint64_t o_text = cv.take<uint8_t>(text->size());
   const uint64_t o_len = cv.take<uint64_t>(o->n_units);
+  const uint64_t o_psrc = cv.take<uint64_t>(o->n_units);
   const uint64_t o_end = cv.take<uint64_t>(o->n_units);
   const uint64_t o_tmp = cv.take<uint8_t>(o->scan_bytes);
   const uint64_t o_out = cv.take<uint8_t>(o->cap);
@@ -2172,6 +2174,7 @@ int magot_fasta_text_create(magot_ctx* ctx, const magot_gffplan* gp, const magot
   o->roff = reinterpret_cast<const uint64_t*>(base + o_roff);
   o->text = reinterpret_cast<const uint8_t*>(base + o_text);
   o->len = reinterpret_cast<uint64_t*>(base + o_len);
+  o->psrc = reinterpret_cast<uint64_t*>(base + o_psrc);
   o->end = reinterpret_cast<uint64_t*>(base + o_end);
   o->scan_tmp = base + o_tmp;
   o->out = reinterpret_cast<uint8_t*>(base + o_out);

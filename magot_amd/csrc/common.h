@@ -340,8 +340,8 @@ bool gffplan_units(const magot_gffplan* p, const std::string** text, std::vector
 size_t text_scan_bytes(uint64_t n);
 void launch_text_assembly(const TextUnit* units, uint64_t n, const uint64_t* rspan,
                           const uint8_t* pay, int protein, const uint8_t* text, uint64_t* len,
-                          uint64_t* end, void* scan_tmp, size_t scan_bytes, uint8_t* out,
-                          hipStream_t s);
+                          uint64_t* psrc, uint64_t* end, void* scan_tmp, size_t scan_bytes,
+                          uint8_t* out, hipStream_t s);
 
 // Standard genetic code (genome.py:795-802) as a 64-byte table indexed
 // c0 + 4*c1 + 16*c2 with A=0, C=1, G=2, T=3.

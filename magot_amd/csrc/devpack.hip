@@ -25,6 +25,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include "common.h"
+#include "wavecopy.h"
 
 namespace magot {
 namespace {
@@ -161,23 +162,6 @@ __global__ __launch_bounds__(kPackThreads) void nib_pack_kernel(const uint8_t* _
 // Segment copy
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ uint4 funnel16(uint4 a, uint4 b, uint32_t sh) {
-  // bytes [sh, sh+16) of the 32-byte concatenation a:b (sh wave-uniform)
-  const uint32_t r = 8 * (sh & 3);
-  uint32_t w0, w1, w2, w3, w4;
-  switch (sh >> 2) {
-    case 0: w0 = a.x; w1 = a.y; w2 = a.z; w3 = a.w; w4 = b.x; break;
-    case 1: w0 = a.y; w1 = a.z; w2 = a.w; w3 = b.x; w4 = b.y; break;
-    case 2: w0 = a.z; w1 = a.w; w2 = b.x; w3 = b.y; w4 = b.z; break;
-    default: w0 = a.w; w1 = b.x; w2 = b.y; w3 = b.z; w4 = b.w; break;
-  }
-  if (!r) return make_uint4(w0, w1, w2, w3);
-  return make_uint4(__builtin_amdgcn_alignbit(w1, w0, r), __builtin_amdgcn_alignbit(w2, w1, r),
-                    __builtin_amdgcn_alignbit(w3, w2, r), __builtin_amdgcn_alignbit(w4, w3, r));
-}
-
-constexpr int kCopyUnroll = 4;
-
 __global__ __launch_bounds__(256) void segments_copy_kernel(const uint8_t* __restrict__ src,
                                                             const uint64_t* __restrict__ src_off,
                                                             const uint64_t* __restrict__ dst_off,
@@ -186,43 +170,7 @@ __global__ __launch_bounds__(256) void segments_copy_kernel(const uint8_t* __res
   const uint64_t seg = (uint64_t)blockIdx.x * 4 +
                        (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / 64);
   if (seg >= n) return;
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t d0 = dst_off[seg], d1 = dst_off[seg + 1], s0 = src_off[seg];
-  if (d1 <= d0) return;
-  const uint64_t a = (d0 + 15) & ~15ull, b = d1 & ~15ull;
-  // partial chunks: [d0, min(a, d1)) and, when a <= b, [b, d1)
-  const uint64_t head_end = a < d1 ? a : d1;
-  if (lane < 16) {
-    const uint64_t p = d0 + lane;
-    if (p < head_end) dst[p] = src[s0 + (p - d0)];
-  } else if (lane < 32 && a <= b) {
-    const uint64_t p = b + (lane - 16);
-    if (p < d1) dst[p] = src[s0 + (p - d0)];
-  }
-  if (a >= b) return;
-  // full chunks [a, b): the source of chunk A is s0 + (A - d0); every aligned
-  // 16-byte block read holds a byte of the segment, so it is inside the
-  // source allocation
-  const uint64_t sa = s0 + (a - d0);
-  const uint32_t sh = (uint32_t)(sa & 15);
-  const uint8_t* sbase = src + (sa & ~15ull);
-  const uint64_t nchunks = (b - a) >> 4;
-  for (uint64_t c0 = 0; c0 < nchunks; c0 += 64 * kCopyUnroll) {
-    uint4 lo[kCopyUnroll], hi[kCopyUnroll];
-#pragma unroll
-    for (int k = 0; k < kCopyUnroll; ++k) {
-      const uint64_t c = c0 + lane + 64 * k;
-      if (c < nchunks) {
-        lo[k] = *reinterpret_cast<const uint4*>(sbase + 16 * c);
-        hi[k] = sh ? *reinterpret_cast<const uint4*>(sbase + 16 * c + 16) : lo[k];
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kCopyUnroll; ++k) {
-      const uint64_t c = c0 + lane + 64 * k;
-      if (c < nchunks) *reinterpret_cast<uint4*>(dst + a + 16 * c) = funnel16(lo[k], hi[k], sh);
-    }
-  }
+  wave_copy_span(src, src_off[seg], dst, dst_off[seg], dst_off[seg + 1], threadIdx.x & 63);
 }
 
 }  // namespace
