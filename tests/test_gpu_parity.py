@@ -977,3 +977,33 @@ def test_device_text_assembly_obiroi():
     assert got == host
     want = _json('fixtures.json')['obiroi/protein/py2']
     assert _sha(got + b'\n') == want['sha256']  # fixture: get_fasta + '\n'
+
+
+@pytest.mark.parametrize('seq_type', ['nucleotide', 'protein'])
+def test_device_text_assembly_tiny_units(seq_type):
+    """Many units per 16-byte chunk and per 16-unit group: CDS of 1-40 bases,
+    blank genes, long IDs, both strands -- every partial-chunk and group-edge
+    case of text_copy_kernel against the host render and the oracle.  (Protein
+    CDS keep 3+ bases: shorter records take the reference's None path, which
+    the native planner hands to the object path.)"""
+    rng = np.random.default_rng(11)
+    lo_len = 0 if seq_type == 'nucleotide' else 2
+    fasta = '>c1\n' + ''.join(rng.choice(list('ACGTacgtN'), 20000)) + '\n'
+    rows = []
+    for g in range(700):
+        lo = 1 + int(rng.integers(0, 19000))
+        gid = 'g%d' % g + ('x' * int(rng.integers(0, 40)) if g % 5 == 0 else '')
+        rows.append('c1\tx\tgene\t%d\t%d\t.\t+\t.\tID=%s' % (lo, lo + 900, gid))
+        if g % 3 == 0:
+            continue  # blank record
+        s = '+-'[int(rng.integers(0, 2))]
+        rows.append('c1\tx\tmRNA\t%d\t%d\t.\t%s\t.\tID=m%d;Parent=%s' % (lo, lo + 900, s, g, gid))
+        for k in range(1 + int(rng.integers(0, 3))):
+            a = lo + 60 * k
+            rows.append('c1\tx\tCDS\t%d\t%d\t.\t%s\t0\tID=cds%d_%d;Parent=m%d'
+                        % (a, a + int(rng.integers(lo_len, 40)), s, g, k, g))
+    gff = '\n'.join(rows) + '\n'
+    got, host = _device_text(fasta, gff, seq_type)
+    assert got == host
+    want = mo.gff2fasta(fasta, gff, seq_type=seq_type, order='py2')
+    assert got + b'\n' == want.encode('latin-1')
