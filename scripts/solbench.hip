@@ -305,6 +305,20 @@ int main(int argc, char** argv) {
                                             nuc, pep, per, xrun); },
                    nm, (double)ntiles * (nuc + pep), 0.0);
         }
+    for (int nt = 1; nt >= 0; --nt) {
+      // the nucleotide stream alone (no residue stream interleaved)
+      const int g = (int)((ntiles + 3) / 4);
+      if (nt)
+        timeit([&] { hipLaunchKernelGGL(c3_stores<true>, g, 256, pad, 0, o1, o2, ntiles, nuc, 0u,
+                                        1u, 16u); },
+               "stores: nucleotide stream only, nt", (double)ntiles * nuc, 0.0);
+      else
+        timeit([&] { hipLaunchKernelGGL(c3_stores<false>, g, 256, pad, 0, o1, o2, ntiles, nuc, 0u,
+                                        1u, 16u); },
+               "stores: nucleotide stream only, plain", (double)ntiles * nuc, 0.0);
+    }
+    timeit([&] { (void)hipMemsetAsync(o1, 7, (uint64_t)ntiles * nuc); },
+           "hipMemset of the nucleotide bytes", (double)ntiles * nuc, 0.0);
     {
       // one flat grid-stride fill of the same bytes (what a library memset does)
       CK(hipMemsetAsync(o1, 7, (uint64_t)ntiles * nuc));
