@@ -68,8 +68,10 @@ def main():
     ph['gff_read_and_plan_native'] = time.perf_counter() - t
     assert plan is not None
     t = time.perf_counter()
+    # as the CLI builds it: records laid out in genome order for the text assembly
     ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
-                               engine.OUT_PEP if protein else engine.OUT_NUC)
+                               (engine.OUT_PEP if protein else engine.OUT_NUC)
+                               | engine.OUT_GENOME_ORDER)
     ph['plan_h2d'] = time.perf_counter() - t
     t = time.perf_counter()
     ex.execute()
