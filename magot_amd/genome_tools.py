@@ -159,12 +159,11 @@ def _gff2fasta_run(genome_sequence, dev, plan, plan_gff):
         if plan is None:
             return None, seqs
     try:
-        # the device text assembly reads each record where the plan laid it
-        # out, so the extraction runs in genome order (neighbouring loci in
-        # neighbouring tiles); host renders keep record order
+        # record order: the CLI launches once, so the genome-order layout's
+        # ~12 us off the kernel would cost ~60 ms more planning on the host
+        # (profiles/r05/text_assembly/)
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
-                                   (engine.OUT_PEP if plan.protein else engine.OUT_NUC)
-                                   | (0 if plan.n_select else engine.OUT_GENOME_ORDER))
+                                   engine.OUT_PEP if plan.protein else engine.OUT_NUC)
         if plan.n_select:
             # longest=True over peptides: the render picks from the trimmed
             # lengths, on the host
@@ -380,8 +379,7 @@ def _flank_native(genome_sequence, gff, sequence_length, stream, feature_type, n
     try:
         if len(plan.txs) == 0:
             return b''
-        ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
-                                   engine.OUT_NUC | engine.OUT_GENOME_ORDER)
+        ex = engine.ExtractionPlan(dev, plan.exons, plan.txs, engine.OUT_NUC)
         text = engine.FastaText(plan, ex)
         try:
             ex.execute()

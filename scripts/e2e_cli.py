@@ -32,6 +32,8 @@ def main():
     ap.add_argument('--whole', action='store_true',
                     help='time the CLI call (genome_tools._gff2fasta_native) on the files of '
                          'an earlier run, in this fresh process, and compare with its out.fa')
+    ap.add_argument('--layout', default='record', choices=['record', 'genome'],
+                    help='extraction plan layout for the phase run')
     a = ap.parse_args()
     os.makedirs(a.dir, exist_ok=True)
     fa, gf = os.path.join(a.dir, 'genome.fa'), os.path.join(a.dir, 'ann.gff3')
@@ -68,10 +70,11 @@ def main():
     ph['gff_read_and_plan_native'] = time.perf_counter() - t
     assert plan is not None
     t = time.perf_counter()
-    # as the CLI builds it: records laid out in genome order for the text assembly
+    # as the CLI builds it (record order: one launch does not repay the
+    # genome-order layout's extra planning; --layout genome to compare)
     ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                (engine.OUT_PEP if protein else engine.OUT_NUC)
-                               | engine.OUT_GENOME_ORDER)
+                               | (engine.OUT_GENOME_ORDER if a.layout == 'genome' else 0))
     ph['plan_h2d'] = time.perf_counter() - t
     t = time.perf_counter()
     ex.execute()
