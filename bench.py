@@ -622,6 +622,14 @@ def run_job(args, dist, rank, local, world):
     n_b2b = max(20, min(args.steps, 100))
     kernel_b2b = timer.time_b2b(n_b2b)
     kernel_iso = timer.time(10)
+    kernel_rec = None
+    if outputs & engine.OUT_GENOME_ORDER:
+        # beside it, for transparency: the same job in record order (the
+        # layout the reference's output has), back-to-back launches
+        rp = engine.ExtractionPlan(dev, ex, tx, outputs & ~engine.OUT_GENOME_ORDER)
+        rp.time_b2b(20)
+        kernel_rec = rp.time_b2b(n_b2b)
+        rp.close()
     kernel_ms_max = allreduce_max(dist, kernel_ms)
     # per-rank figures of a shared job (where a scaling loss sits: the slowest
     # rank's kernel, or the host's time around it)
@@ -741,6 +749,7 @@ def run_job(args, dist, rank, local, world):
                          'kernel_ms_b2b_source': 'HIP events around %d back-to-back launches '
                                                  'after the timed region' % n_b2b,
                          'kernel_ms_isolated': kernel_iso,
+                         'kernel_ms_b2b_record_layout': kernel_rec,
                          'timed_launches': {'kernel': kernel_name, 'first': launches_before,
                                             'count': args.steps,
                                             'note': 'dispatch indices of this kernel in the '
