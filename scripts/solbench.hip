@@ -139,6 +139,26 @@ __global__ __launch_bounds__(256) void c3_stores(uint8_t* nuc, uint8_t* pep, uin
   }
 }
 
+// flat store streams over one buffer (what a fill kernel does): grid-stride
+// 16-byte stores, consecutive lanes on consecutive chunks (kLanes64 false), or
+// each lane writing 64 consecutive bytes as four stores (true)
+template <bool kLanes64, bool kNt>
+__global__ __launch_bounds__(256) void flat_stores(uint8_t* p, uint64_t chunks) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  if (!kLanes64) {
+    for (uint64_t c = tid; c < chunks; c += nthr)
+      st16(p + 16 * c, kNt ? make_uint4((uint32_t)c, 1, 2, 3)
+                           : make_uint4(0x07070707u, 0x07070707u, 0x07070707u, 0x07070707u),
+           kNt);
+  } else {
+    for (uint64_t c = 4 * tid; c < chunks; c += 4 * nthr)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < chunks) st16(p + 16 * (c + k), make_uint4((uint32_t)c, k, 2, 3), kNt);
+  }
+}
+
 struct C5Args {
   const uint8_t* plane;
   uint64_t plane_lines;
@@ -319,6 +339,21 @@ int main(int argc, char** argv) {
     }
     timeit([&] { (void)hipMemsetAsync(o1, 7, (uint64_t)ntiles * nuc); },
            "hipMemset of the nucleotide bytes", (double)ntiles * nuc, 0.0);
+    {
+      const uint64_t ch = (uint64_t)ntiles * nuc / 16;
+      for (int blocks : {256 * 6, 256 * 8, 256 * 32, 1000, 1280, 1792, 2560, 3000, 3072, 4096, 5000, 12000}) {
+        char nm[96];
+        snprintf(nm, sizeof nm, "flat: lane-contiguous, %d blocks, nt", blocks);
+        timeit([&] { hipLaunchKernelGGL((flat_stores<false, true>), blocks, 256, 0, 0, o1, ch); },
+               nm, (double)ntiles * nuc, 0.0);
+        snprintf(nm, sizeof nm, "flat: lane-contiguous, %d blocks, plain, constant bytes", blocks);
+        timeit([&] { hipLaunchKernelGGL((flat_stores<false, false>), blocks, 256, 0, 0, o1, ch); },
+               nm, (double)ntiles * nuc, 0.0);
+        snprintf(nm, sizeof nm, "flat: 64 B per lane, %d blocks, plain", blocks);
+        timeit([&] { hipLaunchKernelGGL((flat_stores<true, false>), blocks, 256, 0, 0, o1, ch); },
+               nm, (double)ntiles * nuc, 0.0);
+      }
+    }
     {
       // one flat grid-stride fill of the same bytes (what a library memset does)
       CK(hipMemsetAsync(o1, 7, (uint64_t)ntiles * nuc));
