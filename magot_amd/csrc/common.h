@@ -333,6 +333,9 @@ struct TextUnit {
   uint32_t text_len;
   uint32_t rec;  // record index, or kNoRecord
 };
+// Record indices in ascending key order, ties in index order (pack.cpp;
+// magot_plan_create's genome-order layout).  key.size() < 2^32.
+void radix_order(const std::vector<uint64_t>& key, std::vector<uint32_t>* out);
 // The planner's skeleton as units (consecutive text pieces merged).
 // Returns false when a record index does not fit a TextUnit.
 bool gffplan_units(const magot_gffplan* p, const std::string** text, std::vector<TextUnit>* units,

@@ -205,4 +205,24 @@ void pack_genome(const ContigSource* src, uint32_t n, HostPacked* out) {
   exc_runs_directory(out);
 }
 
+// --- planner helper (host) ---------------------------------------------------
+
+// Record indices in ascending key order, ties in index order: an LSD radix
+// sort in 11-bit digits, as many passes as the largest key needs.
+void radix_order(const std::vector<uint64_t>& key, std::vector<uint32_t>* out) {
+  const uint64_t n = key.size();
+  uint64_t top = 0;
+  for (uint64_t k : key) top = std::max(top, k);
+  std::vector<uint32_t> a(n), b(n);
+  for (uint64_t i = 0; i < n; ++i) a[i] = (uint32_t)i;
+  for (int shift = 0; shift < 64 && (top >> shift); shift += 11) {
+    std::vector<uint64_t> cnt(2049, 0);
+    for (uint64_t i = 0; i < n; ++i) ++cnt[((key[a[i]] >> shift) & 2047) + 1];
+    for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
+    for (uint64_t i = 0; i < n; ++i) b[cnt[(key[a[i]] >> shift) & 2047]++] = a[i];
+    a.swap(b);
+  }
+  out->swap(a);
+}
+
 }  // namespace magot

@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void c3_stores(uint8_t* nuc, uint8_t* pep, uin
     if (t >= ntiles) return;
     uint8_t* const n0 = nuc + t * nuc_bytes;
 #pragma unroll
-    for (int s = 0; s < 5; ++s) {
+    for (int s = 0; s < 8; ++s) {
       const uint32_t c = 64 * s + lane;
       if (16 * c < nuc_bytes) st16(n0 + 16 * c, make_uint4(c, s, (uint32_t)t, 1), kNt);
     }
@@ -325,6 +325,16 @@ int main(int argc, char** argv) {
                                             nuc, pep, per, xrun); },
                    nm, (double)ntiles * (nuc + pep), 0.0);
         }
+    for (uint32_t tb : {3024u, 4096u, 4608u, 5056u, 5072u, 5120u, 5632u, 6144u, 7168u}) {
+      // the nucleotide stream alone at other tile sizes (XCD runs of 16 blocks, nt)
+      const uint32_t nt_tiles = (uint32_t)((uint64_t)ntiles * nuc / tb);
+      const int g = (int)((nt_tiles + 3) / 4);
+      char nm[96];
+      snprintf(nm, sizeof nm, "stores: nucleotide stream only, %u-byte tiles", tb);
+      timeit([&] { hipLaunchKernelGGL(c3_stores<true>, g, 256, pad, 0, o1, o2, nt_tiles, tb, 0u,
+                                      1u, 16u); },
+             nm, (double)nt_tiles * tb, 0.0);
+    }
     for (int nt = 1; nt >= 0; --nt) {
       // the nucleotide stream alone (no residue stream interleaved)
       const int g = (int)((ntiles + 3) / 4);

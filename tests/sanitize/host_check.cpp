@@ -13,6 +13,7 @@
 // Exit status 0 = every input processed (ASan/UBSan abort on the first
 // finding with a report on stderr); the packer's output is also checked
 // against a scalar restatement of the nibble layout (common.h HostPacked).
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -384,6 +385,27 @@ static void synthetic_packs() {
   check_pack(std::vector<ContigSource>{one});
 }
 
+// magot_plan_create's genome-order layout: radix_order against std::stable_sort
+// (empty, one record, equal keys, small / wide / sparse key ranges)
+static void synthetic_orders() {
+  Rng rng(7);
+  const uint64_t sizes[] = {0, 1, 2, 17, 4096, 100003};
+  const uint64_t ranges[] = {1, 3, 2048, 2049, 1ull << 22, 1ull << 40, ~0ull};
+  for (uint64_t n : sizes)
+    for (uint64_t range : ranges) {
+      std::vector<uint64_t> key(n);
+      for (uint64_t i = 0; i < n; ++i) key[i] = range == ~0ull ? rng.next() : rng.below(range);
+      std::vector<uint32_t> got;
+      radix_order(key, &got);
+      std::vector<uint32_t> want(n);
+      for (uint64_t i = 0; i < n; ++i) want[i] = (uint32_t)i;
+      std::stable_sort(want.begin(), want.end(),
+                       [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+      CHECK(got == want, "radix_order n=%llu range=%llu differs from stable_sort",
+            (unsigned long long)n, (unsigned long long)range);
+    }
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: host_check LIST [mutations]\n");
@@ -432,6 +454,7 @@ int main(int argc, char** argv) {
     }
   }
   synthetic_packs();
+  synthetic_orders();
   printf("host_check: %d fasta, %d gff (%d plans, %d flank plans, %d mutated gff), %d cds "
          "inputs; %d check failure(s)\n", n_fa, n_gff, planned, flanks, n_mutated, n_cds,
          g_failures);
