@@ -1139,7 +1139,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     return MAGOT_OK;
   };
   // the large tile, or the small one for translating plans too small to fill
-  // the chip several times over (MAGOT_EXTRACT_LANE_CHUNKS=3|5 forces one, for
+  // the chip several times over (MAGOT_EXTRACT_LANE_CHUNKS=3|6 forces one, for
   // A/Bs); nucleotide-only plans keep the large tile (C2: 0.0164 vs 0.0172 ms)
   uint32_t lane_chunks = kLaneChunksLarge;
   if (int rc = cut(tile_bytes(kLaneChunksLarge))) return rc;

@@ -133,15 +133,20 @@ void launch_wire_unpack(const uint32_t* code2, const uint32_t* mask, uint64_t n_
 constexpr int kThreads = 256;                 // one workgroup = 4 independent waves
 constexpr int kWaves = kThreads / 64;
 constexpr int kChunk = 16;                    // bytes per lane-store
-// Chunk slots per lane per tile: 5 (5072-byte tiles) for large plans; 3
+// Chunk slots per lane per tile: 6 (6096-byte tiles) for large plans; 3
 // (3024-byte tiles) for translating plans too small to fill the chip several
 // times over (one GPU's share of an 8-GPU C4 job: -3.5 % per launch; 4-GPU
-// share -2.7 %; but the 2-GPU share +8 %, C2 (nucleotides only) +5.5 %, and at
-// full C3 size 4 slots are +3.6 % slower; A/Bs in EXPERIMENTS.md §3).
-constexpr int kLaneChunksLarge = 5, kLaneChunksSmall = 3;
+// share -2.7 %; but the 2-GPU share +8 %, C2 (nucleotides only) +5.5 %;
+// EXPERIMENTS.md §3).  Full C3: 6 slots -2.5 to -3.1 % against 5 (a tile's
+// fixed chain of dependent loads paid 17 % less often; 77 VGPRs, 26.4 KB LDS
+// per block, still 6 blocks per CU), 7 slots (with 3 residue chunks per lane)
+// no better than 5 (89 VGPRs: 5 blocks per CU), 4 slots +3.6 %
+// (profiles/r05/large_tile/).
+constexpr int kLaneChunksLarge = 6, kLaneChunksSmall = 3;
 // Output bytes of a tile cut for `lane_chunks` slots per lane (3 slots of halo):
-// 5072 for the large tile (<= 1691 residues, <= 106 residue chunks), 3024 for
-// the small one.  Size any per-tile storage with the template's LC.
+// 6096 for the large tile (<= 2032 residues, <= 127 residue chunks: within
+// kPepSlots), 3024 for the small one.  Size any per-tile storage with the
+// template's LC.
 constexpr int tile_bytes(int lane_chunks) { return (64 * lane_chunks - 3) * 16; }
 // plans whose large-tile count is below this use the small tile
 constexpr uint64_t kSmallTilePlan = 40000;

@@ -13,7 +13,7 @@
 // Work decomposition (output-stationary, HBM-bound):
 //   * The host cuts the concatenated nucleotide output into 16-byte aligned
 //     tiles of <= tile_bytes(LC) bytes, LC = the chunk slots per lane the plan
-//     was cut for (5: 5072 bytes = 317 chunks of 16 for large plans; 3: 3024
+//     was cut for (6: 6096 bytes = 381 chunks of 16 for large plans; 3: 3024
 //     bytes for translating plans under kSmallTilePlan tiles; shorter where a
 //     tile would touch more than kExonCap intervals or kTxCap records).  A
 //     tile belongs to ONE wavefront: 64 lanes x LC chunk slots (the tile's

@@ -18,7 +18,7 @@ ORDER = engine.OUT_GENOME_ORDER
 BOTH = engine.OUT_NUC | engine.OUT_PEP
 
 
-@pytest.fixture(autouse=True, params=['auto', '5'])
+@pytest.fixture(autouse=True, params=['auto', '6'])
 def tile_size(request, monkeypatch):
     """Both extraction tile sizes (see test_gpu_parity.tile_size)."""
     if request.param == 'auto':

@@ -34,11 +34,11 @@ def _sha(s):
     return hashlib.sha256(s).hexdigest()
 
 
-@pytest.fixture(autouse=True, params=['auto', '5'])
+@pytest.fixture(autouse=True, params=['auto', '6'])
 def tile_size(request, monkeypatch):
     """Every test under both extraction tile sizes: 'auto' (test-size plans
     take the small 3-slot tile, full-size ones the large tile) and the large
-    5-slot tile forced (magot_plan_create reads MAGOT_EXTRACT_LANE_CHUNKS)."""
+    6-slot tile forced (magot_plan_create reads MAGOT_EXTRACT_LANE_CHUNKS)."""
     if request.param == 'auto':
         monkeypatch.delenv('MAGOT_EXTRACT_LANE_CHUNKS', raising=False)
     else:
