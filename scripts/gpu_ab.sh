@@ -22,7 +22,7 @@ for v in base var; do
   lib=magot_amd/libmagot.so; [ $v = var ] && lib=$VAR
   for grp in FETCH_SIZE WRITE_SIZE; do
     rm -rf $OUT/pmc_$v/$grp
-    MAGOT_LIB=$lib timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_$v/$grp -o pmc -- python bench.py --config $CFG --steps 5 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline --no-box-state > $OUT/pmc_$v.$grp.log 2>&1 || { echo "pmc $v $grp failed"; tail -3 $OUT/pmc_$v.$grp.log; exit 1; }
+    MAGOT_LIB=$lib timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc_$v/$grp -o pmc -- python bench.py --config $CFG --steps 5 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline --no-box-state --no-layout-compare > $OUT/pmc_$v.$grp.log 2>&1 || { echo "pmc $v $grp failed"; tail -3 $OUT/pmc_$v.$grp.log; exit 1; }
   done
 done
 echo done

@@ -146,7 +146,7 @@ if has pmc; then
              "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
     i=$((i+1))
     rm -rf $OUT/pmc$i
-    timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python bench.py --steps 5 --warmup 1 --no-verify --no-cpu-baseline --no-box-state > $OUT/pmc$i.log 2>&1
+    timeout -k 10 600 rocprofv3 --pmc $grp --output-format csv -d $OUT/pmc$i -o pmc -- python bench.py --steps 5 --warmup 1 --no-verify --no-cpu-baseline --no-box-state --no-layout-compare > $OUT/pmc$i.log 2>&1
     rc=$?
     if [ $rc -ne 0 ]; then echo "pmc group $i failed rc=$rc"; tail -3 $OUT/pmc$i.log; [ $rc -ge 124 ] && exit 1; fi
   done
@@ -159,7 +159,7 @@ if has traffic; then
     c=${cfg%%:*}
     for grp in FETCH_SIZE WRITE_SIZE; do
       rm -rf $OUT/traffic_$c/$grp
-      timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/traffic_$c/$grp -o pmc -- python bench.py --config $c --steps 5 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline --no-box-state > $OUT/traffic_$c.$grp.log 2>&1 || { echo "traffic $c $grp failed"; tail -3 $OUT/traffic_$c.$grp.log; exit 1; }
+      timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/traffic_$c/$grp -o pmc -- python bench.py --config $c --steps 5 --warmup 1 --settle-ms 0 --no-verify --no-cpu-baseline --no-box-state --no-layout-compare > $OUT/traffic_$c.$grp.log 2>&1 || { echo "traffic $c $grp failed"; tail -3 $OUT/traffic_$c.$grp.log; exit 1; }
     done
   done
   echo traffic ok
