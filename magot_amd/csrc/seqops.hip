@@ -492,7 +492,8 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
                              (uint32_t)(A & 31u) | ((rw[h].y & kOrf6ExcRow) ? 32u : 0u),
                              (uint32_t)rel[h], (uint32_t)(A >> 5) << 2);
     }
-    reinterpret_cast<uint4*>(cnt)[lane] = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) cnt[kPer * lane + i] = 0u;  // vectors kPer lane .. + kPer-1
     const uint32_t m = (uint32_t)(__popcll(__ballot(in[0])) + __popcll(__ballot(in[1])));
     __builtin_amdgcn_wave_barrier();
     // first interval of every vector: count interval starts per vector
@@ -506,11 +507,13 @@ __global__ __launch_bounds__(kOpsThreads, 6) void orf6_kernel(Orf6Args a) {
     }
     __builtin_amdgcn_wave_barrier();
     {
-      const uint4 c = reinterpret_cast<const uint4*>(cnt)[lane];  // vectors 4 lane .. + 3
-      const uint32_t c0 = c.x, c1 = c0 + c.y, c2 = c1 + c.z, c3 = c2 + c.w;
-      const uint32_t x = wave_scan(c3);
-      const uint32_t base = x - c3 - 1;
-      reinterpret_cast<uint4*>(cnt)[lane] = make_uint4(base + c0, base + c1, base + c2, base + c3);
+      uint32_t c[kPer];  // running counts of vectors kPer lane .. + kPer-1
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) c[i] = cnt[kPer * lane + i] + (i ? c[i - 1] : 0u);
+      const uint32_t x = wave_scan(c[kPer - 1]);
+      const uint32_t base = x - c[kPer - 1] - 1;
+#pragma unroll
+      for (int i = 0; i < kPer; ++i) cnt[kPer * lane + i] = base + c[i];
     }
     __builtin_amdgcn_wave_barrier();
     // Codon indices straight from the 2-bit code plane: translation ignores
