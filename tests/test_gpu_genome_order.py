@@ -5,6 +5,8 @@ record order -- byte for byte what the record-order plan returns, which the
 rest of the GPU suite pins to the oracle (the C3 case here checks against the
 C oracle directly).  Needs an MI355X: ``pytest -m gpu``."""
 
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -85,7 +87,7 @@ def _same_as_record_order(dev, ex, tx, outputs=BOTH):
         bns, bps = base.layout()
         assert np.array_equal(bns, want[1][:-1]) and np.array_equal(bps, want[3][:-1])
         # the device buffers hold each record at its place
-        nptr, pptr = ctypes_outputs(plan)
+        nptr, pptr = _device_outputs(plan)
         for ptr_, total, start, off, ref in ((nptr, plan.nuc_bytes, ns.astype(np.int64), noff, want[0]),
                                              (pptr, plan.pep_bytes, ps.astype(np.int64), poff, want[2])):
             if ref is None or not total:
@@ -111,8 +113,8 @@ def _same_as_record_order(dev, ex, tx, outputs=BOTH):
         base.close()
 
 
-def ctypes_outputs(plan):
-    import ctypes
+def _device_outputs(plan):
+    """The plan's device output buffers (magot_plan_device_outputs)."""
     n, p = ctypes.c_void_p(), ctypes.c_void_p()
     _lib.check(_lib.lib().magot_plan_device_outputs(plan.handle, ctypes.byref(n),
                                                     ctypes.byref(p)), 'magot_plan_device_outputs')
