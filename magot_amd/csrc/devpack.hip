@@ -19,9 +19,9 @@
 // Reassembly (magot_copy_segments): after an RCCL gather of every
 // rank's outputs into one buffer, dst is the job's output in global record
 // order, a concatenation of n segments each copied from anywhere in src.
-// One wave per segment: 16-byte aligned destination chunks, the source read
-// as two aligned 16-byte blocks and funnel-shifted by the segment's (uniform)
-// misalignment; the partial chunks at the segment's two ends byte by byte.
+// One wave per group of 16 segments (wavecopy.h span_group_copy): whole
+// 16-byte destination chunks from funnel-shifted pairs of aligned 16-byte
+// source blocks, the partial chunks at the segments' ends byte by byte.
 #include <rocprim/device/device_scan.hpp>
 
 #include "common.h"
@@ -162,15 +162,29 @@ __global__ __launch_bounds__(kPackThreads) void nib_pack_kernel(const uint8_t* _
 // Segment copy
 // ---------------------------------------------------------------------------
 
+// one wave per group of kSpanGroup consecutive segments (their destinations
+// are one contiguous range: dst_off is a prefix table)
 __global__ __launch_bounds__(256) void segments_copy_kernel(const uint8_t* __restrict__ src,
                                                             const uint64_t* __restrict__ src_off,
                                                             const uint64_t* __restrict__ dst_off,
                                                             uint64_t n, uint8_t* __restrict__ dst) {
-  // segment index: the block part stays 64-bit outside readfirstlane (32 bits)
-  const uint64_t seg = (uint64_t)blockIdx.x * 4 +
-                       (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / 64);
-  if (seg >= n) return;
-  wave_copy_span(src, src_off[seg], dst, dst_off[seg], dst_off[seg + 1], threadIdx.x & 63);
+  __shared__ SpanGroup lds[4];
+  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t s0 = ((uint64_t)blockIdx.x * 4 + wv) * kSpanGroup;
+  if (s0 >= n) return;
+  const uint32_t m = (uint32_t)(n - s0 < kSpanGroup ? n - s0 : kSpanGroup);
+  SpanGroup& L = lds[wv];
+  if (lane < m) {
+    const uint64_t o = dst_off[s0 + lane];
+    L.o[lane] = o;
+    L.te[lane] = o;  // no text parts
+    L.toff[lane] = 0;
+    L.src[lane] = src_off[s0 + lane];
+    if (lane == m - 1) L.o[m] = dst_off[s0 + m];
+  }
+  __builtin_amdgcn_wave_barrier();
+  span_group_copy(L, m, src, src, dst, lane);  // no text parts: `text` is never read
 }
 
 }  // namespace
@@ -217,7 +231,8 @@ void launch_nib_pack(const uint8_t* raw, uint64_t n, uint32_t* nib, uint64_t nib
 void launch_segments_copy(const uint8_t* src, const uint64_t* src_off, const uint64_t* dst_off,
                           uint64_t n, uint8_t* dst, hipStream_t s) {
   if (!n) return;
-  hipLaunchKernelGGL(segments_copy_kernel, dim3((uint32_t)((n + 3) / 4)), dim3(256), 0, s, src,
+  const uint64_t groups = (n + kSpanGroup - 1) / kSpanGroup;
+  hipLaunchKernelGGL(segments_copy_kernel, dim3((uint32_t)((groups + 3) / 4)), dim3(256), 0, s, src,
                      src_off, dst_off, n, dst);
 }
 
