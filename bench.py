@@ -33,6 +33,7 @@ Rank 0 prints ONE JSON line (contract in DESIGN.md).
 """
 
 import argparse
+import faulthandler
 import json
 import os
 import signal
@@ -42,6 +43,11 @@ import sys
 import time
 
 import numpy as np
+
+# a native crash in any thread (HIP runtime, RCCL, c10d's store and watchdog
+# threads) prints every thread's Python stack to stderr before the process
+# dies (a SIGSEGV during --dist start-up left no record)
+faulthandler.enable(all_threads=True)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -124,26 +130,108 @@ def spawn_ranks(n, argv, script=None):
     return rc
 
 
+def dist_init_kwargs(backend, rank, world, device, env=None):
+    """The ``init_process_group`` arguments of this rank, spelled out:
+      * ``init_method`` an explicit tcp:// URL on MASTER_ADDR (127.0.0.1 by
+        default, never a name to resolve: c10d's lookup of the box's hostname
+        fails there, err=-3) and MASTER_PORT, with rank and world size given,
+        instead of env:// discovery (under torchrun the agent's store is still
+        the one joined: torch's tcp:// handler honours it);
+      * ``device_id`` the rank's device under nccl: the process group is bound
+        to it and RCCL's communicator is created eagerly, inside this call on
+        the main thread, instead of lazily inside the first collective.
+    ``device`` is the rank's device index (None without a GPU)."""
+    import datetime
+    env = os.environ if env is None else env
+    kw = {'backend': backend,
+          'init_method': 'tcp://%s:%s' % (env.get('MASTER_ADDR') or '127.0.0.1',
+                                          env['MASTER_PORT']),
+          'rank': rank, 'world_size': world,
+          'timeout': datetime.timedelta(seconds=float(env.get('MAGOT_DIST_TIMEOUT_S', '900')))}
+    if backend == 'nccl' and device is not None:
+        import torch
+        kw['device_id'] = torch.device('cuda', device)
+    return kw
+
+
+def rccl_log_env(rank, env=None):
+    """NCCL_DEBUG=INFO (subsystem INIT) into one file per rank, so a multi-GPU
+    run leaves RCCL's own init record (nranks, rings / channels, "Init
+    COMPLETE"); summarised into the JSON line by ``rccl_init_summary``.  Set
+    before the communicator exists.  MAGOT_RCCL_LOG=0 turns it off; a caller's
+    own NCCL_DEBUG settings win.  Returns the file (None when off)."""
+    env = os.environ if env is None else env
+    if env.get('MAGOT_RCCL_LOG', '1') == '0' or 'NCCL_DEBUG_FILE' in env:
+        return env.get('NCCL_DEBUG_FILE')
+    d = os.path.join(env.get('TMPDIR') or '/tmp', 'magot_rccl_%s' % env.get('MASTER_PORT', '0'))
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, 'rank%d.log' % rank)
+    env.setdefault('NCCL_DEBUG', 'INFO')
+    env.setdefault('NCCL_DEBUG_SUBSYS', 'INIT')
+    env['NCCL_DEBUG_FILE'] = path
+    return path
+
+
+_RCCL_KEYS = ('RCCL version', 'Init START', 'Init COMPLETE', 'Init timings', 'Channel 00/',
+              'Connected all rings')
+
+
+def rccl_init_summary(path, max_lines=10):
+    """The init lines of one rank's RCCL log (see ``rccl_log_env``)."""
+    if not path or not os.path.exists(path):
+        return {'file': path, 'lines': []}
+    keep = []
+    with open(path, errors='replace') as fh:
+        for line in fh:
+            if any(k in line for k in _RCCL_KEYS):
+                keep.append(line.strip()[:240])
+                if len(keep) >= max_lines:
+                    break
+    return {'file': path, 'lines': keep}
+
+
+_RCCL_LOG = None  # this rank's RCCL log file (nccl backend)
+
+
 def dist_setup(force=False):
     """The process group of this rank (None for a single rank unless
     ``force``: ``--dist`` runs the multi-rank job's collective path -- the
     genome broadcast, the output gather, the reductions -- through a process
-    group of one rank, RCCL with the nccl backend)."""
+    group of one rank, RCCL with the nccl backend).
+
+    Start-up is ordered so no other thread runs while the HIP runtime comes
+    up: the device is selected and its context created on the main thread
+    first, then the process group (explicit tcp:// URL, ``device_id`` bound:
+    ``dist_init_kwargs``), whose communicator RCCL then creates eagerly."""
+    global _RCCL_LOG
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world == 1 and not force:
         return None, rank, local, world
-    import torch
     import torch.distributed as dist
-    backend = 'gloo'
-    if torch.cuda.is_available():
-        # one GPU per rank; MAGOT_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs
-        torch.cuda.set_device(local % torch.cuda.device_count())
-        backend = 'nccl'            # RCCL on ROCm
+    device = bind_device(local)
+    backend = 'gloo' if device is None else 'nccl'    # nccl: RCCL on ROCm
     backend = os.environ.get('MAGOT_DIST_BACKEND', backend)
-    dist.init_process_group(backend=backend)
+    if backend == 'nccl':
+        _RCCL_LOG = rccl_log_env(rank)
+    dist.init_process_group(**dist_init_kwargs(backend, rank, world, device))
     return dist, rank, local, world
+
+
+def bind_device(local):
+    """Select this rank's GPU (one per rank; MAGOT_DIST_BACKEND=gloo rehearses
+    N ranks on fewer GPUs) and create its context on the calling thread,
+    before any process-group thread exists.  None without a GPU."""
+    import torch
+    if not torch.cuda.is_available():
+        return None
+    device = local % torch.cuda.device_count()
+    torch.cuda.set_device(device)
+    torch.cuda.init()
+    torch.empty(1, device='cuda').zero_()
+    torch.cuda.synchronize()
+    return device
 
 
 def shard_seed(config, rank):
@@ -623,12 +711,18 @@ def run_job(args, dist, rank, local, world):
     kernel_b2b = timer.time_b2b(n_b2b)
     kernel_iso = timer.time(10)
     kernel_rec = None
+    delivery = None
     if outputs & engine.OUT_GENOME_ORDER and not args.no_layout_compare:
         # beside it, for transparency: the same job in record order (the
-        # layout the reference's output has), back-to-back launches
+        # layout the reference's output has), given the same settle and
+        # warm-up as the line's own plan, then timed back to back
         rp = engine.ExtractionPlan(dev, ex, tx, outputs & ~engine.OUT_GENOME_ORDER)
-        rp.time_b2b(20)
+        settle(rp.execute, ctx.sync, args.settle_ms)
+        for _ in range(args.warmup):
+            rp.execute()
+        ctx.sync()
         kernel_rec = rp.time_b2b(n_b2b)
+        delivery = record_order_delivery(plan, rp, ctx, B, P)
         rp.close()
     kernel_ms_max = allreduce_max(dist, kernel_ms)
     # per-rank figures of a shared job (where a scaling loss sits: the slowest
@@ -670,6 +764,11 @@ def run_job(args, dist, rank, local, world):
     rss_all = all_values(dist, rss_gb)
     setup_all = all_values(dist, t_setup - t_wait)
     wait_all = all_values(dist, t_wait)
+    rccl_init = None
+    if dist is not None and dist.get_backend() == 'nccl':
+        # every rank's RCCL init record (NCCL_DEBUG=INFO, subsystem INIT) into the line
+        rccl_init = [None] * world
+        dist.all_gather_object(rccl_init, rccl_init_summary(_RCCL_LOG))
     host = {'peak_rss_gib_max_rank': max(rss_all),
             'peak_rss_gib_rank0': rss_gb,
             'peak_rss_gib_per_rank': rss_all,
@@ -750,6 +849,7 @@ def run_job(args, dist, rank, local, world):
                                                  'after the timed region' % n_b2b,
                          'kernel_ms_isolated': kernel_iso,
                          'kernel_ms_b2b_record_layout': kernel_rec,
+                         'record_order_delivery': delivery,
                          'timed_launches': {'kernel': kernel_name, 'first': launches_before,
                                             'count': args.steps,
                                             'note': 'dispatch indices of this kernel in the '
@@ -781,6 +881,8 @@ def run_job(args, dist, rank, local, world):
             rec['genome_arena_bytes'] = int(dev.device_bytes)
             rec['load_imbalance'] = imb
             rec['outputs_gather'] = gather
+        if rccl_init is not None:
+            rec['rccl_init'] = rccl_init
         print(json.dumps(rec), flush=True)
     if o6 is not None:
         o6.close()
@@ -788,6 +890,40 @@ def run_job(args, dist, rank, local, world):
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def record_order_delivery(plan, rec_plan, ctx, B, P, iters=5):
+    """What a genome-ordered line costs a caller who wants the buffers in
+    record order on the device: ``plan.copy_outputs`` (magot_plan_copy_outputs,
+    one segment copy per record) against the same call on the record-order
+    plan ``rec_plan`` (a plain device-to-device copy), both timed with HIP
+    events on the library's stream.  The FASTA text assembly (gff2fasta)
+    reads the genome-ordered buffers in place and pays neither."""
+    import torch
+    nuc = torch.empty(max(B, 1), dtype=torch.uint8, device='cuda')
+    pep = torch.empty(max(P, 1), dtype=torch.uint8, device='cuda')
+    torch.cuda.synchronize()
+    na, pa = nuc.data_ptr(), (pep.data_ptr() if P else None)
+
+    def timed(p):
+        p.copy_outputs(na, pa)
+        ctx.mark(0)
+        for _ in range(iters):
+            p.copy_outputs(na, pa)
+        ctx.mark(1)
+        ctx.sync()
+        return ctx.elapsed_ms() / iters
+
+    reassemble = timed(plan)
+    plain = timed(rec_plan)
+    del nuc, pep
+    torch.cuda.empty_cache()
+    return {'reassemble_ms': reassemble, 'plain_d2d_copy_ms': plain,
+            'extra_ms': reassemble - plain,
+            'note': 'record-order device buffers: magot_plan_copy_outputs on the genome-ordered '
+                    'plan (segment copies) vs on the record-order plan (plain D2D copy); once '
+                    'per job, outside the step; gff2fasta\'s device text assembly reads the '
+                    'genome-ordered buffers in place'}
 
 
 def gather_outputs(args, dist, rank, world, w, plan, o6, shards, ctx):

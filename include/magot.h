@@ -234,8 +234,9 @@ int magot_genome_wire_import(magot_ctx* ctx, const uint8_t* meta, uint64_t meta_
  * both 16-byte aligned (else MAGOT_ERR_ARG),
  * dst_off has n+1 non-decreasing entries, the offset tables are host arrays;
  * a segment reaching past src_bytes is refused (MAGOT_ERR_RANGE) before any
- * launch.  Synchronous.  No reference counterpart (the reference is
- * single-process).
+ * launch, and so is a segment of 4 GiB or more (MAGOT_ERR_ARG: the grouped
+ * copy counts 16-byte chunks in 32 bits; split such a segment).  Synchronous.
+ * No reference counterpart (the reference is single-process).
  */
 int magot_copy_segments(magot_ctx* ctx, const void* src_dev, uint64_t src_bytes, void* dst_dev,
                         const uint64_t* src_off, const uint64_t* dst_off, uint64_t n);
@@ -272,7 +273,10 @@ int magot_ctx_elapsed(magot_ctx* ctx, double* ms);
 int magot_ctx_info(const magot_ctx* ctx, int* n_cu, int* extract_blocks_per_cu);
 
 /* Copy outputs to caller buffers (synchronous).  Any pointer may be NULL to
- * skip it.  nuc_off / pep_off receive n_tx+1 prefix offsets. */
+ * skip it.  nuc_off / pep_off receive n_tx+1 prefix offsets.  A plan built
+ * with MAGOT_OUT_GENOME_ORDER is put back into record order on the device on
+ * the way down, through a transient device scratch of at most 256 MiB (or
+ * the longest record, if longer) plus 16 bytes, batch by batch of records. */
 int magot_plan_fetch(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* nuc_off,
                      uint8_t* pep_out, uint64_t* pep_off);
 

@@ -315,12 +315,16 @@ int magot_genome_load(magot_ctx* ctx, const uint8_t* const* seqs, const uint64_t
 namespace {
 
 struct Lap {
-  const bool on = std::getenv("MAGOT_GENOME_TIMING") != nullptr;
+  const char* tag;
+  const bool on;
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit Lap(const char* env = "MAGOT_GENOME_TIMING", const char* tag_ = "genome")
+      : tag(tag_), on(std::getenv(env) != nullptr) {}
   void operator()(const char* what) {
     if (!on) return;
     const auto t1 = std::chrono::steady_clock::now();
-    fprintf(stderr, "[genome] %-8s %.3f s\n", what, std::chrono::duration<double>(t1 - t0).count());
+    fprintf(stderr, "[%s] %-10s %.4f s\n", tag, what,
+            std::chrono::duration<double>(t1 - t0).count());
     t0 = t1;
   }
 };
@@ -402,6 +406,50 @@ int plan_reassemble(magot_ctx* ctx, const magot_plan* p, bool residues, void* ds
                        residues ? p->d_pep_off : p->d_nuc_off, p->n_tx,
                        static_cast<uint8_t*>(dst), ctx->stream);
   MAGOT_HIP_TRY(hipGetLastError());
+  return MAGOT_OK;
+}
+
+// A genome-ordered plan's output copied down in record order through a
+// bounded device scratch: consecutive records in batches of at most
+// kFetchBatchBytes (or one longer record) are put back into record order on
+// the device (one segment-copy launch per batch), then copied to the host.
+// The scratch is 16-byte aligned and the batch's first record keeps its
+// offset mod 16, so the copy kernel's aligned stores stay aligned.
+constexpr uint64_t kFetchBatchBytes = 256ull << 20;
+
+uint64_t fetch_batch_bytes() {  // MAGOT_FETCH_BATCH_BYTES: test hook (small batches)
+  const char* e = std::getenv("MAGOT_FETCH_BATCH_BYTES");
+  const uint64_t v = e ? strtoull(e, nullptr, 10) : 0;
+  return v ? v : kFetchBatchBytes;
+}
+
+int plan_fetch_reordered(magot_ctx* ctx, const magot_plan* p, bool residues, uint8_t* host) {
+  const std::vector<uint64_t>& off = residues ? p->pep_off : p->nuc_off;
+  const uint64_t T = p->n_tx;
+  if (!T || off[T] == 0) return MAGOT_OK;
+  uint64_t longest = 0;
+  for (uint64_t t = 0; t < T; ++t) longest = std::max(longest, off[t + 1] - off[t]);
+  const uint64_t cap = std::max(std::min(off[T], fetch_batch_bytes()), longest);
+  DevBuf scratch;
+  MAGOT_HIP_TRY(hipMalloc(&scratch.p, cap + 16));
+  uint8_t* S = static_cast<uint8_t*>(scratch.p);
+  const uint8_t* src = residues ? p->args.pep : p->args.nuc;
+  const uint64_t* lay = residues ? p->d_lay_pep : p->d_lay_nuc;
+  const uint64_t* doff = residues ? p->d_pep_off : p->d_nuc_off;
+  for (uint64_t r0 = 0; r0 < T;) {
+    uint64_t r1 = r0 + 1;
+    while (r1 < T && off[r1 + 1] - off[r0] <= cap) ++r1;
+    const uint64_t base = off[r0], bytes = off[r1] - base;
+    if (bytes) {
+      // record-order offset x lands at S + (x - (base & ~15))
+      launch_segments_copy(src, lay + r0, doff + r0, r1 - r0, S - (base & ~15ull), ctx->stream);
+      MAGOT_HIP_TRY(hipGetLastError());
+      MAGOT_HIP_TRY(hipMemcpyAsync(host + base, S + (base & 15), bytes, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+    }
+    r0 = r1;
+  }
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   return MAGOT_OK;
 }
 
@@ -918,6 +966,13 @@ int magot_copy_segments(magot_ctx* ctx, const void* src_dev, uint64_t src_bytes,
       set_error("magot_copy_segments: segment " + std::to_string(i) + " reads past src_bytes");
       return MAGOT_ERR_RANGE;
     }
+    // the grouped copy counts a group's 16-byte chunks in 32 bits (wavecopy.h):
+    // below 4 GiB per segment, a group of kSpanGroup stays below 2^32 chunks
+    if (len >> 32) {
+      set_error("magot_copy_segments: segment " + std::to_string(i) +
+                " is 4 GiB or longer (split it)");
+      return MAGOT_ERR_ARG;
+    }
   }
   DevBuf tables;
   MAGOT_HIP_TRY(hipMalloc(&tables.p, (2 * n + 1) * 8));
@@ -951,6 +1006,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     return MAGOT_ERR_ARG;
   }
   *out = nullptr;
+  Lap lap("MAGOT_PLAN_TIMING", "plan");
   const uint64_t E = n_exons, T = n_tx;
   // --- validate and build per-record offsets --------------------------------
   uint64_t expect = 0;
@@ -1013,6 +1069,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   }
   rec_ex[T] = w_g.size();
   const uint64_t Ec = w_g.size();
+  lap("pass1");
   // Layout order of the records: record order, or (MAGOT_OUT_GENOME_ORDER) by
   // the genome position of each record's first non-empty interval (records
   // without output last), so that records sharing genome lines run in
@@ -1025,6 +1082,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
       key[t] = rec_ex[t] < rec_ex[t + 1] ? w_g[rec_ex[t]] & ~kExFlagBits : g->span;
     radix_order(key, &order);
   }
+  lap("order");
   // Pass 2, layout order: the interval table with its output offsets, and
   // each record's place (lay_*, indexed by record)
   std::vector<uint64_t> ex_g, ex_out;
@@ -1065,6 +1123,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   const uint64_t Tc = tn.size();
   tn.push_back(B);
   tp.push_back(P);
+  lap("pass2");
   if (Ec >= 0xFFFFFFFFull || Tc >= 0xFFFFFFFFull) {
     set_error("magot_plan_create: table too large for one plan (split it)");
     return MAGOT_ERR_ARG;
@@ -1075,14 +1134,25 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   // ownership is rounded up to 16-residue (16-byte) store chunks, so nearly
   // every peptide store is a full aligned chunk; the residues a tile owns past
   // its last codon start are decoded from its kHalo bytes of look-ahead.
-  auto pcount = [&](uint64_t T) -> uint64_t {  // residues whose codon starts before T
-    const uint64_t j = std::upper_bound(tn.begin(), tn.begin() + Tc, T) - tn.begin();
+  // Every query below is monotone over the cut (tile ends, decode ends and
+  // residue bounds only grow), so the searches are cursors that move forward:
+  // O(records + tiles) per cut instead of a binary search per query.
+  struct Cursor {  // upper_bound over a non-decreasing table, for non-decreasing queries
+    const uint64_t* v;
+    uint64_t n, j;
+    uint64_t operator()(uint64_t x) {
+      while (j < n && v[j] <= x) ++j;
+      return j;
+    }
+  };
+  auto pcount = [&](Cursor& c, uint64_t T) -> uint64_t {  // residues whose codon starts before T
+    const uint64_t j = c(T);
     if (j == 0) return 0;
     const uint64_t into = T - tn[j - 1];
     return tp[j - 1] + std::min((into + 2) / 3, tp[j] - tp[j - 1]);
   };
-  auto rec_of = [&](uint64_t q) -> uint64_t {  // compacted record holding residue q < P
-    return (std::upper_bound(tp.begin(), tp.begin() + Tc, q) - tp.begin()) - 1;
+  auto rec_of = [&](Cursor& c, uint64_t q) -> uint64_t {  // compacted record holding residue q < P
+    return c(q) - 1;
   };
   std::vector<uint64_t> tile_start, tile_q;
   std::vector<uint32_t> tile_ex, tile_tx;
@@ -1092,11 +1162,13 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     tile_q.clear();
     tile_ex.clear();
     tile_tx.clear();
+    Cursor c_end{tn.data(), Tc, 0}, c_dec{tn.data(), Tc, 0};    // pcount(T1), pcount(dec_end - 2)
+    Cursor c_r0{tp.data(), Tc, 0}, c_r1{tp.data(), Tc, 0};      // rec_of(R0), rec_of(R1 - 1)
     uint64_t e1 = 0, e2 = 0;
     uint64_t T0 = 0, R0 = 0;
     while (T0 < B) {
       while (e1 < Ec && ex_out[e1 + 1] <= T0) ++e1;           // interval containing T0
-      const uint64_t j1 = R0 < P ? rec_of(R0) : Tc;            // record holding residue R0
+      const uint64_t j1 = R0 < P ? rec_of(c_r0, R0) : Tc;      // record holding residue R0
       uint64_t T1 = std::min<uint64_t>(T0 + tile, B);
       if (e1 + kExonCap < Ec) T1 = std::min<uint64_t>(T1, ex_out[e1 + kExonCap] - kHalo);
       if (j1 + kTxCap - kChunk < Tc) T1 = std::min<uint64_t>(T1, tn[j1 + kTxCap - kChunk]);
@@ -1110,16 +1182,17 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
       // but only codons that end inside the decoded range and at most kPepSlots chunks
       uint64_t R1 = P;
       if (T1 < B) {
-        R1 = std::min<uint64_t>((pcount(T1) + kChunk - 1) & ~(uint64_t)(kChunk - 1), P);
-        R1 = std::min<uint64_t>(R1, pcount(dec_end - 2));
+        R1 = std::min<uint64_t>((pcount(c_end, T1) + kChunk - 1) & ~(uint64_t)(kChunk - 1), P);
+        R1 = std::min<uint64_t>(R1, pcount(c_dec, dec_end - 2));
         R1 = std::min<uint64_t>(R1, (R0 & ~(uint64_t)(kChunk - 1)) + kPepSlots * kChunk);
       }
       if (R1 < R0) R1 = R0;
       if (e2 < e1) e2 = e1;
       while (e2 < Ec && ex_out[e2] < dec_end) ++e2;           // intervals touching the decode range
-      const uint64_t j2 = R1 > R0 ? rec_of(R1 - 1) + 1 : j1;  // records holding residues [R0, R1)
+      const uint64_t jl = R1 > R0 ? rec_of(c_r1, R1 - 1) : 0;  // record holding the last residue
+      const uint64_t j2 = R1 > R0 ? jl + 1 : j1;               // records holding residues [R0, R1)
       if (e2 - e1 > (uint64_t)kExonCap || (R1 > R0 && j2 - j1 > (uint64_t)kTxCap) ||
-          (R1 > R0 && tn[rec_of(R1 - 1)] + 3 * (R1 - 1 - tp[rec_of(R1 - 1)]) + 3 > dec_end)) {
+          (R1 > R0 && tn[jl] + 3 * (R1 - 1 - tp[jl]) + 3 > dec_end)) {
         set_error("magot_plan_create: internal tiling error");
         return MAGOT_ERR_STATE;
       }
@@ -1153,6 +1226,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   }
   tile_start.push_back(B);
   tile_q.push_back(P);
+  lap("tiles");
   const uint64_t n_tiles64 = tile_start.size() - 1;
   if (n_tiles64 >= 0x7FFFFFFFull) {
     set_error("magot_plan_create: output too large for one launch");
@@ -1178,6 +1252,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     else tail.push_back(r);
   }
   std::copy(tail.begin(), tail.end(), tiles.begin() + n_first);
+  lap("launch_ord");
 
   // --- device arena -----------------------------------------------------------
   std::unique_ptr<magot_plan> p(new magot_plan());
@@ -1205,6 +1280,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   const uint64_t o_rec_pep = cv.take<uint64_t>(by_genome ? T + 1 : 0);
   MAGOT_HIP_TRY(hipMalloc(&p->arena, cv.used));
   p->arena_bytes = cv.used;
+  lap("malloc");
   char* base = static_cast<char*>(p->arena);
   auto up = [&](uint64_t off, const void* src, uint64_t bytes) -> hipError_t {
     if (!bytes) return hipSuccess;
@@ -1226,6 +1302,7 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     p->d_lay_pep = reinterpret_cast<const uint64_t*>(base + o_lay_pep);
     p->d_pep_off = reinterpret_cast<const uint64_t*>(base + o_rec_pep);
   }
+  lap("upload");
 
   ExtractArgs& a = p->args;
   a.nib = g->nib;
@@ -1303,35 +1380,24 @@ int magot_plan_fetch(magot_ctx* ctx, magot_plan* p, uint8_t* nuc_out, uint64_t* 
               (nuc_out && !(p->args.outputs & MAGOT_OUT_NUC) ? "MAGOT_OUT_NUC" : "MAGOT_OUT_PEP"));
     return MAGOT_ERR_STATE;
   }
-  // a genome-ordered plan's outputs are put back into record order on the
-  // device first (one segment copy into a scratch buffer), then copied down
-  DevBuf scratch;
   const bool want_nuc = nuc_out && p->args.total_nuc, want_pep = pep_out && p->args.total_pep;
-  if (p->genome_order && (want_nuc || want_pep)) {
-    MAGOT_HIP_TRY(hipMalloc(&scratch.p, std::max(want_nuc ? p->args.total_nuc : 0,
-                                                 want_pep ? p->args.total_pep : 0)));
-  }
   if (want_nuc) {
-    const void* src = p->args.nuc;
     if (p->genome_order) {
-      if (int rc = plan_reassemble(ctx, p, false, scratch.p)) return rc;
-      src = scratch.p;
+      if (int rc = plan_fetch_reordered(ctx, p, false, nuc_out)) return rc;
+    } else {
+      MAGOT_HIP_TRY(hipMemcpyAsync(nuc_out, p->args.nuc, p->args.total_nuc,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+      MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
-    // on the context stream, behind the reassembly copy (a non-blocking stream)
-    MAGOT_HIP_TRY(hipMemcpyAsync(nuc_out, src, p->args.total_nuc, hipMemcpyDeviceToHost,
-                                 ctx->stream));
-    MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   }
   if (want_pep) {
-    const void* src = p->args.pep;
     if (p->genome_order) {
-      if (int rc = plan_reassemble(ctx, p, true, scratch.p)) return rc;
-      src = scratch.p;
+      if (int rc = plan_fetch_reordered(ctx, p, true, pep_out)) return rc;
+    } else {
+      MAGOT_HIP_TRY(hipMemcpyAsync(pep_out, p->args.pep, p->args.total_pep,
+                                   hipMemcpyDeviceToHost, ctx->stream));
+      MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
     }
-    // on the context stream, behind the reassembly copy (a non-blocking stream)
-    MAGOT_HIP_TRY(hipMemcpyAsync(pep_out, src, p->args.total_pep, hipMemcpyDeviceToHost,
-                                 ctx->stream));
-    MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
   }
   if (nuc_off) std::memcpy(nuc_off, p->nuc_off.data(), p->nuc_off.size() * 8);
   if (pep_off) std::memcpy(pep_off, p->pep_off.data(), p->pep_off.size() * 8);

@@ -156,9 +156,11 @@ __global__ __launch_bounds__(kWireThreads) void wire_unpack_kernel(UnpackArgs a)
   uint32_t w[4] = {spread2(c.x), spread2(c.x >> 16), spread2(c.y), spread2(c.y >> 16)};
 
   // soft-mask: the first run ending past lo lies in [mdir[blk], mdir[blk+1]]
+  // (directory entries clamped to the run count: a corrupt image whose header
+  // matches the genome reads no run past the list's sentinel)
   {
-    uint64_t r0 = a.mdir[blk];
-    uint64_t r1 = blk + 1 < a.n_mdir ? a.mdir[blk + 1] : a.n_mask;
+    uint64_t r0 = min((uint64_t)a.mdir[blk], a.n_mask);
+    uint64_t r1 = blk + 1 < a.n_mdir ? min((uint64_t)a.mdir[blk + 1], a.n_mask) : a.n_mask;
     while (r0 < r1) {
       const uint64_t mid = (r0 + r1) >> 1;
       if ((uint64_t)a.mask[2 * mid + 1] > lo) r1 = mid; else r0 = mid + 1;
@@ -175,8 +177,9 @@ __global__ __launch_bounds__(kWireThreads) void wire_unpack_kernel(UnpackArgs a)
   // exceptions: the literal class of every byte outside ACGTacgt (nibble 8 | class)
   const uint32_t d = a.edir[blk];
   if (!(d & kDirClean)) {
-    uint64_t r0 = d & ~kDirClean;
-    uint64_t r1 = blk + 1 < a.n_edir ? (a.edir[blk + 1] & ~kDirClean) : a.n_exc;
+    uint64_t r0 = min((uint64_t)(d & ~kDirClean), a.n_exc);
+    uint64_t r1 = blk + 1 < a.n_edir ? min((uint64_t)(a.edir[blk + 1] & ~kDirClean), a.n_exc)
+                                     : a.n_exc;
     while (r0 < r1) {
       const uint64_t mid = (r0 + r1) >> 1;
       if (a.exc[mid].start + a.exc[mid].len > lo) r1 = mid; else r0 = mid + 1;

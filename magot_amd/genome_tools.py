@@ -23,12 +23,43 @@ Python-3 order.
 
 import ast
 import ctypes
+import json
+import os
 import sys
+import time
 
 import numpy as np
 
 from . import engine
 from . import genome
+
+
+class _Clock(object):
+    """Wall-clock phases of one CLI call, from the call's start: with
+    MAGOT_CLI_TIMING=1 one JSON line on stderr (``{"cli_phases_s": ...}``);
+    otherwise nothing is recorded.  ``at(name)`` stamps the time since the
+    start (any thread); ``lap(name)`` the time since the previous lap."""
+
+    def __init__(self):
+        self.on = os.environ.get('MAGOT_CLI_TIMING') == '1'
+        self.t0 = self.last = time.perf_counter()
+        self.laps, self.stamps = {}, {}
+
+    def lap(self, name):
+        if self.on:
+            t = time.perf_counter()
+            self.laps[name] = self.laps.get(name, 0.0) + t - self.last
+            self.last = t
+
+    def at(self, name):
+        if self.on:
+            self.stamps[name] = time.perf_counter() - self.t0
+
+    def emit(self):
+        if self.on:
+            sys.stderr.write(json.dumps({'cli_phases_s': self.laps, 'cli_stamps_s': self.stamps,
+                                         'cli_total_s': time.perf_counter() - self.t0}) + '\n')
+            sys.stderr.flush()
 
 
 def _literal(text):
@@ -70,11 +101,14 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
     lg, gm = _literal(longest), _literal(genomic)
     if (native == 'True' and isinstance(lg, bool) and isinstance(gm, bool) and
             seq_type in ('nucleotide', 'protein')):
+        clock = _Clock()
         text, parsed = _gff2fasta_native(genome_sequence, gff, seq_type, order,
                                          longest=lg is True, genomic=gm is True,
-                                         from_exons=from_exons == 'True')
+                                         from_exons=from_exons == 'True', clock=clock)
         if text is not None:
             _write_bytes(text, b'\n')
+            clock.lap('write')
+            clock.emit()
             return
         if parsed is not None:
             genome_sequence = parsed  # read once: the object path reuses it
@@ -90,7 +124,7 @@ def gff2fasta(genome_sequence, gff, from_exons='False', seq_type='nucleotide', l
 
 
 def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, genomic=False,
-                      from_exons=False):
+                      from_exons=False, clock=None):
     """(text, parsed): the gff2fasta text (bytes) via the native planner, the
     extraction kernel and device text assembly, or (None, GenomeSequence or
     None) when it declines -- the GenomeSequence already parsed, for the
@@ -98,6 +132,7 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
     if order not in ('py2', 'insertion'):
         raise ValueError("order must be 'insertion' or 'py2'")
     protein = seq_type == 'protein'
+    clock = clock or _Clock()
 
     def plan_gff(names, lengths):
         return engine.GffPlan.build(genome.read_buffer(gff), names, lengths, protein=protein,
@@ -110,13 +145,26 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
     # uploads and packs the genome (both native calls release the GIL).
     from concurrent.futures import ThreadPoolExecutor
     fa = genome.read_buffer(genome_sequence)
+    clock.lap('fasta_map')
+
+    def load(text):
+        clock.at('load_thread_start')
+        from . import _lib
+        ctx = _lib.default_context()          # device start-up
+        clock.at('device_context_ready')
+        g = engine.FastaGenome.load(text, ctx=ctx)
+        clock.at('genome_on_device')
+        return g
+
     with ThreadPoolExecutor(1) as pool:
-        loading = pool.submit(engine.FastaGenome.load, fa)
+        loading = pool.submit(load, fa)
         plan = None
         try:
             index = engine.fasta_contigs(fa)  # the same reader as the load
+            clock.lap('fasta_index')
             if index is not None:
                 plan = plan_gff(*index)
+                clock.lap('gff_read_and_plan')
         except BaseException:
             # the genome may already be on the device: free it before raising
             try:
@@ -132,6 +180,7 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
             if plan is not None:
                 plan.close()
             raise
+        clock.lap('wait_genome')
     owned = dev  # the FastaGenome this call loaded (closed on every return)
     if dev is None and plan is not None:  # above one device plane
         plan.close()
@@ -140,13 +189,13 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
         dev.close()
         return None, None
     try:
-        return _gff2fasta_run(genome_sequence, dev, plan, plan_gff)
+        return _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock)
     finally:
         if owned is not None:
             owned.close()
 
 
-def _gff2fasta_run(genome_sequence, dev, plan, plan_gff):
+def _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock):
     seqs = None
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)
@@ -164,6 +213,7 @@ def _gff2fasta_run(genome_sequence, dev, plan, plan_gff):
         # (profiles/r05/text_assembly/)
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
                                    engine.OUT_PEP if plan.protein else engine.OUT_NUC)
+        clock.lap('plan_create')
         if plan.n_select:
             # longest=True over peptides: the render picks from the trimmed
             # lengths, on the host
@@ -172,10 +222,15 @@ def _gff2fasta_run(genome_sequence, dev, plan, plan_gff):
             finally:
                 ex.close()
         text = engine.FastaText(plan, ex)
+        clock.lap('text_create')
         try:
             ex.execute()
             text.execute()  # records + headers + joiners in one device buffer
-            return text.fetch(), None
+            ex.sync()
+            clock.lap('kernel_and_text_assembly')
+            out = text.fetch()
+            clock.lap('text_d2h')
+            return out, None
         finally:
             text.close()
             ex.close()

@@ -103,6 +103,11 @@ def imbalance(load):
     return float(load.max() / max(load.mean(), 1e-300) - 1.0) if len(load) else 0.0
 
 
+# where the library's outputs (and so a Gather's send buffer) live; the CPU
+# tests of the collective sequence set 'cpu'
+OUTPUT_DEVICE = 'cuda'
+
+
 def collective_device(dist):
     """Where collective operands live: the device with nccl (RCCL moves
     device memory over xGMI), host memory with gloo.  MAGOT_COLLECTIVE_TENSORS=cuda
@@ -112,7 +117,6 @@ def collective_device(dist):
     if dist.get_backend() == 'nccl' or os.environ.get('MAGOT_COLLECTIVE_TENSORS') == 'cuda':
         return 'cuda'
     return 'cpu'
-
 
 
 def replicate_genome(dist, rank, contigs, ctx, root_replica=False):
@@ -187,9 +191,10 @@ class Gather(object):
     numpy arrays, ``received()`` the whole buffer on the device (for
     ``reassemble_device``)."""
 
-    def __init__(self, dist, rank, world, nbytes, device='cuda'):
+    def __init__(self, dist, rank, world, nbytes, device=None):
         import torch
         self.dist, self.rank, self.world = dist, rank, world
+        device = OUTPUT_DEVICE if device is None else device
         where = collective_device(dist)
         self.staged = where != 'cuda'
         sizes = torch.tensor([int(nbytes)], dtype=torch.int64, device=where)

@@ -39,13 +39,16 @@ def main():
     fa, gf = os.path.join(a.dir, 'genome.fa'), os.path.join(a.dir, 'ann.gff3')
     if a.whole:
         from magot_amd import genome_tools
+        clock = genome_tools._Clock()
+        clock.on = True
         t = time.perf_counter()
-        text = genome_tools._gff2fasta_native(fa, gf, a.seq_type, a.order)[0]
+        text = genome_tools._gff2fasta_native(fa, gf, a.seq_type, a.order, clock=clock)[0]
         total = time.perf_counter() - t
         with open(os.path.join(a.dir, 'out.fa'), 'rb') as fh:
             same = fh.read() == bytes(text) + b'\n'
         print(json.dumps({'config': a.config, 'seq_type': a.seq_type, 'order': a.order,
-                          'cli_call_s': total, 'equals_phase_run_output': same}), flush=True)
+                          'cli_call_s': total, 'equals_phase_run_output': same,
+                          'phases_s': clock.laps, 'stamps_s': clock.stamps}), flush=True)
         return
     t = time.perf_counter()
     w = synth.make(a.config)

@@ -18,6 +18,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
 
+def _failure(r):
+    """A failed child's exit, with a signal named (a native crash: bench.py's
+    fault handler has printed every thread's stack into the stderr tail)."""
+    import signal
+    what = 'exit status %d' % r.returncode
+    if r.returncode < 0:
+        try:
+            what = 'killed by %s' % signal.Signals(-r.returncode).name
+        except ValueError:
+            what = 'killed by signal %d' % -r.returncode
+    return '%s; stderr tail:\n%s' % (what, r.stderr[-6000:])
+
+
 def _bench(args, env_extra=None):
     env = dict(os.environ)
     for k in ('WORLD_SIZE', 'MAGOT_DIST_BACKEND', 'MAGOT_COLLECTIVE_TENSORS'):
@@ -25,7 +38,7 @@ def _bench(args, env_extra=None):
     env.update(env_extra or {})
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env,
                        capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _failure(r)
     lines = [x for x in r.stdout.splitlines() if x.startswith('{')]
     assert len(lines) == 1, r.stdout
     return json.loads(lines[0])
@@ -119,3 +132,6 @@ def test_bench_dist_one_rank_rccl(config):
     # the 2-bit replica image (+ meta), not the 1-byte-per-base arena
     assert d['genome_broadcast_bytes'] < 0.35 * d['genome_arena_bytes'], d['genome_replica']
     assert d['roofline']['kernel'] == ('orf6_kernel' if config == 'small5' else 'extract_kernel')
+    # RCCL's own init record travels in the line (NCCL_DEBUG=INFO, INIT, per rank)
+    lines = d['rccl_init'][0]['lines']
+    assert any('Init COMPLETE' in x and 'nranks 1' in x for x in lines), d['rccl_init']

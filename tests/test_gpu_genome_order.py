@@ -165,6 +165,31 @@ def _edge_tables(w):
     return ex, tx
 
 
+@pytest.mark.parametrize('batch', ['1', '37', '4096'])
+def test_genome_order_fetch_in_bounded_batches(monkeypatch, batch):
+    """magot_plan_fetch of a genome-ordered plan reassembles through a bounded
+    scratch, batch by batch of records (MAGOT_FETCH_BATCH_BYTES; a record
+    longer than the batch is a batch of its own, odd batch starts keep the
+    copy's 16-byte alignment): byte for byte the record-order fetch."""
+    monkeypatch.setenv('MAGOT_FETCH_BATCH_BYTES', batch)
+    w = synth.make('small')
+    dev = engine.DeviceGenome(w.contigs())
+    try:
+        ex, tx = w.plan_tables()
+        base, want = _run(dev, ex, tx, BOTH)
+        plan, got = _run(dev, ex, tx, BOTH | ORDER)
+        try:
+            for a, b in zip(got, want):
+                assert np.array_equal(a, b)
+        finally:
+            plan.close()
+            base.close()
+        ex2, tx2 = _edge_tables(w)
+        _same_as_record_order(dev, ex2, tx2)
+    finally:
+        dev.close()
+
+
 def test_genome_order_edge_records():
     w = synth.make('small')
     dev = engine.DeviceGenome(w.contigs())
