@@ -158,15 +158,18 @@ def rccl_log_env(rank, env=None):
     """NCCL_DEBUG=INFO (subsystem INIT) into one file per rank, so a multi-GPU
     run leaves RCCL's own init record (nranks, rings / channels, "Init
     COMPLETE"); summarised into the JSON line by ``rccl_init_summary``.  Set
-    before the communicator exists.  MAGOT_RCCL_LOG=0 turns it off; a caller's
-    own NCCL_DEBUG settings win.  Returns the file (None when off)."""
+    before the communicator exists.  MAGOT_RCCL_LOG=0 turns it off, and a
+    caller's own NCCL_DEBUG_FILE wins; a level below INFO is raised to INFO
+    (the pool's boxes preset NCCL_DEBUG=VERSION, whose banner then lands in
+    the file instead of on rank 0's stdout).  Returns the file (None when off)."""
     env = os.environ if env is None else env
     if env.get('MAGOT_RCCL_LOG', '1') == '0' or 'NCCL_DEBUG_FILE' in env:
         return env.get('NCCL_DEBUG_FILE')
     d = os.path.join(env.get('TMPDIR') or '/tmp', 'magot_rccl_%s' % env.get('MASTER_PORT', '0'))
     os.makedirs(d, exist_ok=True)
     path = os.path.join(d, 'rank%d.log' % rank)
-    env.setdefault('NCCL_DEBUG', 'INFO')
+    if env.get('NCCL_DEBUG', '').upper() in ('', 'VERSION', 'WARN', 'ABORT'):
+        env['NCCL_DEBUG'] = 'INFO'
     env.setdefault('NCCL_DEBUG_SUBSYS', 'INIT')
     env['NCCL_DEBUG_FILE'] = path
     return path

@@ -452,6 +452,21 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
                    const uint64_t* contig_lens, uint32_t n_contigs, const char* feature,
                    uint32_t flags, magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx);
 /*
+ * magot_gff_plan in two steps, so the GFF can be read before the genome's
+ * contig names are known (gff2fasta reads the GFF while another thread
+ * loads the FASTA): magot_gff_read is read_gff (genome.py:242-415; flags:
+ * MAGOT_GFF_FROM_EXONS is the only one it looks at), magot_gff_lower the
+ * get_fasta lowering against the contigs (the other flags, as above; once
+ * per plan, else MAGOT_ERR_STATE).  `gff` must stay valid until
+ * magot_gff_lower returns.  Either returns MAGOT_ERR_UNSUPPORTED for a
+ * diagnostic path; the plan handle from magot_gff_read is then still the
+ * caller's to destroy.
+ */
+int magot_gff_read(const char* gff, uint64_t gff_len, uint32_t flags, magot_gffplan** out);
+int magot_gff_lower(magot_gffplan* p, const char* const* seqids, const uint64_t* contig_lens,
+                    uint32_t n_contigs, const char* feature, uint32_t flags, uint64_t* n_exons,
+                    uint64_t* n_tx);
+/*
  * extract_upstream_downstream (genome_tools.py:457-480) as a plan of the same
  * shape: one single-interval record per printed window (the `sequence_length`
  * bases before a '+' feature for stream "up", after it reverse-complemented

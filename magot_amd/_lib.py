@@ -34,7 +34,8 @@ EXPORTS = (
     'magot_plan_algorithmic_bytes',
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
     'magot_codon_symbols', 'magot_revcomp', 'magot_translate',
-    'magot_gff_plan', 'magot_flank_plan', 'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
+    'magot_gff_plan', 'magot_gff_read', 'magot_gff_lower', 'magot_flank_plan',
+    'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
     'magot_gffplan_selections', 'magot_cds_scan', 'magot_cds_render',
     'magot_genome_export', 'magot_genome_copy_arena', 'magot_genome_attach',
     'magot_plan_copy_outputs',
@@ -48,6 +49,10 @@ EXPORTS = (
     'magot_genome_wire_export', 'magot_genome_wire_import',
 )
 
+ERR_ARG = -1
+ERR_HIP = -2
+ERR_RANGE = -3
+ERR_STATE = -4
 ERR_UNSUPPORTED = -5
 GFF_PROTEIN = 1
 GFF_ORDER_PY2 = 2
@@ -112,6 +117,11 @@ def _declare(lib):
                                           ctypes.POINTER(ctypes.c_char_p), _u64p, ctypes.c_uint32,
                                           ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(_vp),
                                           _u64p, _u64p]),
+        'magot_gff_read': (ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint32,
+                                          ctypes.POINTER(_vp)]),
+        'magot_gff_lower': (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_char_p), _u64p,
+                                           ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                           _u64p, _u64p]),
         'magot_flank_plan': (ctypes.c_int, [_vp, ctypes.c_uint64,
                                             ctypes.POINTER(ctypes.c_char_p), _u64p,
                                             ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p,

@@ -69,8 +69,10 @@ struct magot_genome {
 struct magot_plan {
   magot_ctx* ctx = nullptr;
   const magot_genome* g = nullptr;
-  void* arena = nullptr;
+  void* arena = nullptr;       // tables (intervals, records, tiles, layout)
   uint64_t arena_bytes = 0;
+  void* out_arena = nullptr;   // output buffers (nucleotides, residues)
+  uint64_t out_bytes = 0;
   ExtractArgs args{};
   std::vector<uint64_t> nuc_off, pep_off;  // host copies, n_tx+1 (record order)
   // MAGOT_OUT_GENOME_ORDER: records laid out in genome order; each record's
@@ -340,19 +342,90 @@ unsigned host_threads() {
   return std::min(hw, 16u);
 }
 
+// fn(lo, hi, part) over `parts` contiguous ranges of [0, n), part 0 on the
+// calling thread; fn must not throw.
+template <class F>
+void parallel_ranges(uint64_t n, unsigned parts, F fn) {
+  if (parts <= 1 || n < 2) {
+    fn(0, n, 0u);
+    return;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(parts - 1);
+  for (unsigned k = 1; k < parts; ++k)
+    pool.emplace_back([&fn, n, parts, k]() { fn(n * k / parts, n * (k + 1) / parts, k); });
+  fn(0, n / parts, 0u);
+  for (std::thread& th : pool) th.join();
+}
+
+// A host array left uninitialised (POD rows the planner writes itself, in
+// parallel: no sequential zero fill, and its pages fault in on the writing threads).
+template <class T>
+struct HostBuf {
+  std::unique_ptr<T[]> p;
+  uint64_t n = 0;
+  explicit HostBuf(uint64_t count = 0) : p(count ? new T[count] : nullptr), n(count) {}
+  T& operator[](uint64_t i) { return p[i]; }
+  const T& operator[](uint64_t i) const { return p[i]; }
+  T* data() { return p.get(); }
+  const T* data() const { return p.get(); }
+};
+
+// Host rows bound for one device allocation (dev_off into it).
+struct HostPiece {
+  uint64_t dev_off;
+  const void* src;
+  uint64_t bytes;
+};
+
+constexpr uint64_t kPinRing = 64ull << 20;  // each of the context's two pinned staging buffers
+
+int ensure_pin_ring(magot_ctx* ctx) {  // callers hold ctx->pin_mu
+  for (int k = 0; k < 2; ++k)
+    if (!ctx->pin[k]) {
+      MAGOT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pin[k]), kPinRing,
+                                  hipHostMallocDefault));
+      MAGOT_HIP_TRY(hipEventCreateWithFlags(&ctx->pin_ev[k], hipEventDisableTiming));
+    }
+  return MAGOT_OK;
+}
+
+// Upload host rows through the context's two pinned staging buffers: host
+// threads copy one 64 MiB piece in while the DMA engine drains the other (a
+// pageable hipMemcpy stages through the runtime's own small buffers at a
+// fraction of the link rate).  Synchronous: the rows are on the device when
+// it returns.
+int upload_pieces(magot_ctx* ctx, char* dev, const std::vector<HostPiece>& pieces) {
+  std::lock_guard<std::mutex> lock(ctx->pin_mu);
+  if (int rc = ensure_pin_ring(ctx)) return rc;
+  const unsigned nt = host_threads();
+  uint64_t k = 0;
+  for (const HostPiece& pc : pieces)
+    for (uint64_t q0 = 0; q0 < pc.bytes; q0 += kPinRing, ++k) {
+      const int b = (int)(k & 1);
+      const uint64_t q1 = std::min(pc.bytes, q0 + kPinRing);
+      MAGOT_HIP_TRY(hipEventSynchronize(ctx->pin_ev[b]));
+      const char* src = static_cast<const char*>(pc.src) + q0;
+      uint8_t* ring = ctx->pin[b];
+      parallel_ranges(q1 - q0, q1 - q0 >= (4ull << 20) ? nt : 1u,
+                      [&](uint64_t lo, uint64_t hi, unsigned) { memcpy(ring + lo, src + lo, hi - lo); });
+      MAGOT_HIP_TRY(hipMemcpyAsync(dev + pc.dev_off + q0, ring, q1 - q0, hipMemcpyHostToDevice,
+                                   ctx->stream));
+      MAGOT_HIP_TRY(hipEventRecord(ctx->pin_ev[b], ctx->stream));
+    }
+  MAGOT_HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return MAGOT_OK;
+}
+
 // Stream the contigs' bytes (FASTA line layout removed) into dev[0, total),
 // total = extent - kOrigin, through two pinned 64 MiB host buffers: host
 // threads fill one while the DMA engine uploads the other.
 int upload_raw(magot_ctx* ctx, const ContigSource* src, const HostPacked& lay, uint8_t* dev) {
   const uint64_t total = lay.extent - kOrigin;
   if (!total) return MAGOT_OK;
-  constexpr uint64_t kRing = 64ull << 20;
+  constexpr uint64_t kRing = kPinRing;
   std::lock_guard<std::mutex> lock(ctx->pin_mu);
-  for (int k = 0; k < 2; ++k)
-    if (!ctx->pin[k]) {
-      MAGOT_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&ctx->pin[k]), kRing, hipHostMallocDefault));
-      MAGOT_HIP_TRY(hipEventCreateWithFlags(&ctx->pin_ev[k], hipEventDisableTiming));
-    }
+  if (int rc = ensure_pin_ring(ctx)) return rc;
   const unsigned nt = host_threads();
   const auto& base = lay.contig_base;
   auto fill = [&](uint8_t* dst, uint64_t x0, uint64_t x1) {  // raw [x0, x1) -> dst
@@ -1027,48 +1100,96 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     return MAGOT_ERR_ARG;
   }
   const uint64_t n_contigs = g->contig_base.size();
+  // Host threads over record ranges for the per-interval passes (a large
+  // plan: C3's 4M intervals); small plans stay on the calling thread.
+  const unsigned nth = T >= (1u << 15) ? host_threads() : 1u;
   // Pass 1, record order: every interval validated, flagged and compacted
   // (zero-length intervals add no output) into words w_g / lengths w_len;
-  // record t's compacted intervals are [rec_ex[t], rec_ex[t+1]).
-  std::vector<uint64_t> w_g;
-  std::vector<uint32_t> w_len;
-  w_g.reserve(E);
-  w_len.reserve(E);
+  // record t's compacted intervals are [rec_ex[t], rec_ex[t+1]).  Two
+  // parallel sweeps: counts (and the first bad interval of each range), then,
+  // after a prefix over the counts, the words.
   std::vector<uint64_t> rec_ex(T + 1), rec_len(T);
-  for (uint64_t t = 0; t < T; ++t) {
-    rec_ex[t] = w_g.size();
-    uint64_t len = 0;
-    const uint64_t e0 = txs[t].exon_begin, e1 = e0 + txs[t].n_exons;
-    for (uint64_t e = e0; e < e1; ++e) {
-      const magot_exon& x = exons[e];
-      const uint64_t st = x.start_rc & ~kRcBit;
-      if (x.contig >= n_contigs || st > g->contig_len[x.contig] ||
-          st + x.len > g->contig_len[x.contig]) {
-        set_error("magot_plan_create: exon " + std::to_string(e) + " outside its contig");
-        return MAGOT_ERR_RANGE;
+  std::vector<uint64_t> first_bad(nth, ~0ull);
+  parallel_ranges(T, nth, [&](uint64_t t0, uint64_t t1, unsigned part) {
+    for (uint64_t t = t0; t < t1; ++t) {
+      uint64_t len = 0, nz = 0;
+      const uint64_t e0 = txs[t].exon_begin, e1 = e0 + txs[t].n_exons;
+      for (uint64_t e = e0; e < e1; ++e) {
+        const magot_exon& x = exons[e];
+        const uint64_t st = x.start_rc & ~kRcBit;
+        if (x.contig >= n_contigs || st > g->contig_len[x.contig] ||
+            st + x.len > g->contig_len[x.contig]) {
+          first_bad[part] = e;
+          return;
+        }
+        len += x.len;
+        nz += x.len != 0;
       }
-      if (x.len == 0) continue;
-      const uint64_t gs = g->contig_base[x.contig] + st;
-      // does [gs, gs+len) touch an exception run?  (dir: first run ending past the block)
-      uint64_t d = g->host_dir[gs >> kDirShift] & ~kDirClean;
-      while (g->host_runs[d].start + g->host_runs[d].len <= gs) ++d;
-      uint64_t exc = g->host_runs[d].start < gs + x.len ? kExcBit : 0;
-      if (exc && !(x.start_rc & kRcBit)) {
-        // forward strand: a byte without a literal class needs the run list
-        for (uint64_t r = d; g->host_runs[r].start < gs + x.len; ++r)
-          if (lit_class(g->host_runs[r].byte) == 7u) {
-            exc |= kSlowLitBit;
-            break;
-          }
-      }
-      w_g.push_back(gs | (x.start_rc & kRcBit) | exc);
-      w_len.push_back(x.len);
-      len += x.len;
+      rec_len[t] = len;
+      rec_ex[t] = nz;
     }
-    rec_len[t] = len;
+  });
+  for (uint64_t e : first_bad)  // ranges ascend: the first bad range holds the first bad interval
+    if (e != ~0ull) {
+      set_error("magot_plan_create: exon " + std::to_string(e) + " outside its contig");
+      return MAGOT_ERR_RANGE;
+    }
+  uint64_t Ec = 0, B = 0, P = 0;
+  for (uint64_t t = 0; t < T; ++t) {
+    const uint64_t c = rec_ex[t];
+    rec_ex[t] = Ec;
+    Ec += c;
+    B += rec_len[t];
+    P += rec_len[t] / 3;
   }
-  rec_ex[T] = w_g.size();
-  const uint64_t Ec = w_g.size();
+  rec_ex[T] = Ec;
+  // The output buffers' size is known now: allocate them on another thread
+  // while this one plans (hipMalloc of C3's 0.8 GB takes ~10 ms).
+  const uint64_t out_nuc = (outputs & MAGOT_OUT_NUC) ? B + 64 : 64;
+  const uint64_t out_pep = (outputs & MAGOT_OUT_PEP) ? P + 64 : 64;
+  const uint64_t out_bytes = ((out_nuc + 255) & ~255ull) + out_pep;
+  void* out_arena = nullptr;
+  hipError_t out_err = hipSuccess;
+  std::thread out_alloc([&]() {
+    out_err = hipSetDevice(ctx->device);
+    if (out_err == hipSuccess) out_err = hipMalloc(&out_arena, out_bytes);
+  });
+  struct JoinFree {  // the allocation is joined, and freed unless the plan took it
+    std::thread& th;
+    void*& mem;
+    ~JoinFree() {
+      if (th.joinable()) th.join();
+      if (mem) (void)hipFree(mem);
+    }
+  } out_guard{out_alloc, out_arena};
+  HostBuf<uint64_t> w_g(Ec + 1);
+  HostBuf<uint32_t> w_len(Ec);
+  parallel_ranges(T, nth, [&](uint64_t t0, uint64_t t1, unsigned) {
+    for (uint64_t t = t0; t < t1; ++t) {
+      uint64_t k = rec_ex[t];
+      const uint64_t e0 = txs[t].exon_begin, e1 = e0 + txs[t].n_exons;
+      for (uint64_t e = e0; e < e1; ++e) {
+        const magot_exon& x = exons[e];
+        if (x.len == 0) continue;
+        const uint64_t gs = g->contig_base[x.contig] + (x.start_rc & ~kRcBit);
+        // does [gs, gs+len) touch an exception run?  (dir: first run ending past the block)
+        uint64_t d = g->host_dir[gs >> kDirShift] & ~kDirClean;
+        while (g->host_runs[d].start + g->host_runs[d].len <= gs) ++d;
+        uint64_t exc = g->host_runs[d].start < gs + x.len ? kExcBit : 0;
+        if (exc && !(x.start_rc & kRcBit)) {
+          // forward strand: a byte without a literal class needs the run list
+          for (uint64_t r = d; g->host_runs[r].start < gs + x.len; ++r)
+            if (lit_class(g->host_runs[r].byte) == 7u) {
+              exc |= kSlowLitBit;
+              break;
+            }
+        }
+        w_g[k] = gs | (x.start_rc & kRcBit) | exc;
+        w_len[k] = x.len;
+        ++k;
+      }
+    }
+  });
   lap("pass1");
   // Layout order of the records: record order, or (MAGOT_OUT_GENOME_ORDER) by
   // the genome position of each record's first non-empty interval (records
@@ -1083,29 +1204,45 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
     radix_order(key, &order);
   }
   lap("order");
-  // Pass 2, layout order: the interval table with its output offsets, and
-  // each record's place (lay_*, indexed by record)
-  std::vector<uint64_t> ex_g, ex_out;
-  ex_out.reserve(Ec + 1);
+  // Pass 2, layout order: each record's place (lay_*, indexed by record) from
+  // one sweep in layout order, then the interval table with its output
+  // offsets, record ranges in parallel (each record's rows are one block)
   std::vector<uint64_t> lay_nuc(T), lay_pep(T);
-  uint64_t acc = 0, P = 0;
-  if (!by_genome) ex_g.swap(w_g);
-  else ex_g.reserve(Ec);
-  for (uint64_t k = 0; k < T; ++k) {
-    const uint64_t t = by_genome ? order[k] : k;
-    lay_nuc[t] = acc;
-    lay_pep[t] = P;
-    for (uint64_t i = rec_ex[t]; i < rec_ex[t + 1]; ++i) {
-      if (by_genome) ex_g.push_back(w_g[i]);
-      ex_out.push_back(acc);
-      acc += w_len[i];
+  HostBuf<uint64_t> lay_ex(T);
+  {
+    uint64_t acc = 0, q = 0, ek = 0;
+    for (uint64_t k = 0; k < T; ++k) {
+      const uint64_t t = by_genome ? order[k] : k;
+      lay_nuc[t] = acc;
+      lay_pep[t] = q;
+      lay_ex[t] = ek;
+      acc += rec_len[t];
+      q += rec_len[t] / 3;
+      ek += rec_ex[t + 1] - rec_ex[t];
     }
-    P += rec_len[t] / 3;
   }
-  const uint64_t B = acc;
-  ex_out.push_back(B);
+  // interval rows in layout order (the record-order rows themselves when the
+  // layout is record order), one padding row past each table (the kernel
+  // prefetches clamped rows j <= n)
+  HostBuf<uint64_t> ex_perm(by_genome ? Ec + 1 : 0), ex_out(Ec + 2);
+  uint64_t* const ex_g = by_genome ? ex_perm.data() : w_g.data();
+  parallel_ranges(T, nth, [&](uint64_t t0, uint64_t t1, unsigned) {
+    for (uint64_t t = t0; t < t1; ++t) {
+      uint64_t k = lay_ex[t], o = lay_nuc[t];
+      for (uint64_t i = rec_ex[t]; i < rec_ex[t + 1]; ++i, ++k) {
+        if (by_genome) ex_g[k] = w_g[i];
+        ex_out[k] = o;
+        o += w_len[i];
+      }
+    }
+  });
+  ex_g[Ec] = 0;
+  ex_out[Ec] = B;
+  ex_out[Ec + 1] = B;
   // Compacted record table in layout order: records with at least one codon.
   std::vector<uint64_t> tn, tp;
+  tn.reserve(T + 3);
+  tp.reserve(T + 3);
   for (uint64_t k = 0; k < T; ++k) {
     const uint64_t t = by_genome ? order[k] : k;
     if (rec_len[t] >= 3) {
@@ -1239,16 +1376,22 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   // run-list loads then overlap the rest of the launch; at the end of the grid
   // they set its tail (C2: 0.0174 ms with the 23 such tiles where they fall,
   // 0.0151 ms with none).  Every other tile keeps output order.
+  std::vector<uint8_t> slow_tile(n_tiles);
+  parallel_ranges(n_tiles, n_tiles >= (1u << 14) ? nth : 1u, [&](uint64_t t0, uint64_t t1, unsigned) {
+    for (uint64_t t = t0; t < t1; ++t) {
+      bool slow = false;
+      for (uint32_t e = tile_ex[2 * t]; e < tile_ex[2 * t + 1] && !slow; ++e)
+        slow = (ex_g[e] & kSlowLitBit) || ex_out[e + 1] - ex_out[e] < (uint64_t)kChunk;
+      slow_tile[t] = slow;
+    }
+  });
   std::vector<TileRec> tiles(n_tiles);
   std::vector<TileRec> tail;
   uint32_t n_first = 0;
   for (uint32_t t = 0; t < n_tiles; ++t) {
     const TileRec r{tile_start[t], tile_start[t + 1], tile_q[t], tile_q[t + 1],
                     tile_ex[2 * t], tile_ex[2 * t + 1], tile_tx[2 * t], tile_tx[2 * t + 1]};
-    bool slow = false;
-    for (uint32_t e = r.e1; e < r.e2 && !slow; ++e)
-      slow = (ex_g[e] & kSlowLitBit) || ex_out[e + 1] - ex_out[e] < (uint64_t)kChunk;
-    if (slow) tiles[n_first++] = r;
+    if (slow_tile[t]) tiles[n_first++] = r;
     else tail.push_back(r);
   }
   std::copy(tail.begin(), tail.end(), tiles.begin() + n_first);
@@ -1260,8 +1403,6 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   p->g = g;
   Carve cv;
   // one padding row past each table: the kernel prefetches clamped rows j <= n
-  ex_g.push_back(0);
-  ex_out.push_back(B);
   tn.push_back(B);
   tp.push_back(P);
   const uint64_t o_exg = cv.take<uint64_t>(Ec + 1);
@@ -1269,8 +1410,6 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   const uint64_t o_txn = cv.take<uint64_t>(Tc + 2);
   const uint64_t o_txp = cv.take<uint64_t>(Tc + 2);
   const uint64_t o_tiles = cv.take<TileRec>(n_tiles + 1);
-  const uint64_t o_nuc = cv.take<uint8_t>((outputs & MAGOT_OUT_NUC) ? B + 64 : 64);
-  const uint64_t o_pep = cv.take<uint8_t>((outputs & MAGOT_OUT_PEP) ? P + 64 : 64);
   // genome order: {layout place, record-order offsets} per output, for the
   // reassembly copies (magot_plan_fetch / copy_outputs)
   const uint64_t lay_rows = by_genome ? T : 0;
@@ -1280,22 +1419,26 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   const uint64_t o_rec_pep = cv.take<uint64_t>(by_genome ? T + 1 : 0);
   MAGOT_HIP_TRY(hipMalloc(&p->arena, cv.used));
   p->arena_bytes = cv.used;
+  out_alloc.join();
+  MAGOT_HIP_TRY(out_err);
+  p->out_arena = out_arena;
+  p->out_bytes = out_bytes;
+  out_arena = nullptr;  // the plan owns it now
   lap("malloc");
   char* base = static_cast<char*>(p->arena);
-  auto up = [&](uint64_t off, const void* src, uint64_t bytes) -> hipError_t {
-    if (!bytes) return hipSuccess;
-    return hipMemcpy(base + off, src, bytes, hipMemcpyHostToDevice);
-  };
-  MAGOT_HIP_TRY(up(o_exg, ex_g.data(), (Ec + 1) * 8));
-  MAGOT_HIP_TRY(up(o_exo, ex_out.data(), (Ec + 2) * 8));
-  MAGOT_HIP_TRY(up(o_txn, tn.data(), (Tc + 2) * 8));
-  MAGOT_HIP_TRY(up(o_txp, tp.data(), (Tc + 2) * 8));
-  MAGOT_HIP_TRY(up(o_tiles, tiles.data(), tiles.size() * sizeof(TileRec)));
+  std::vector<HostPiece> pieces = {{o_exg, ex_g, (Ec + 1) * 8},
+                                   {o_exo, ex_out.data(), (Ec + 2) * 8},
+                                   {o_txn, tn.data(), (Tc + 2) * 8},
+                                   {o_txp, tp.data(), (Tc + 2) * 8},
+                                   {o_tiles, tiles.data(), tiles.size() * sizeof(TileRec)}};
   if (by_genome) {
-    MAGOT_HIP_TRY(up(o_lay_nuc, lay_nuc.data(), T * 8));
-    MAGOT_HIP_TRY(up(o_rec_nuc, nuc_off.data(), (T + 1) * 8));
-    MAGOT_HIP_TRY(up(o_lay_pep, lay_pep.data(), T * 8));
-    MAGOT_HIP_TRY(up(o_rec_pep, pep_off.data(), (T + 1) * 8));
+    pieces.push_back({o_lay_nuc, lay_nuc.data(), T * 8});
+    pieces.push_back({o_rec_nuc, nuc_off.data(), (T + 1) * 8});
+    pieces.push_back({o_lay_pep, lay_pep.data(), T * 8});
+    pieces.push_back({o_rec_pep, pep_off.data(), (T + 1) * 8});
+  }
+  if (int rc = upload_pieces(ctx, base, pieces)) return rc;
+  if (by_genome) {
     p->genome_order = true;
     p->d_lay_nuc = reinterpret_cast<const uint64_t*>(base + o_lay_nuc);
     p->d_nuc_off = reinterpret_cast<const uint64_t*>(base + o_rec_nuc);
@@ -1314,8 +1457,8 @@ int magot_plan_create(magot_ctx* ctx, const magot_genome* g, const magot_exon* e
   a.tx_nuc = reinterpret_cast<const uint64_t*>(base + o_txn);
   a.tx_pep = reinterpret_cast<const uint64_t*>(base + o_txp);
   a.tiles = reinterpret_cast<const TileRec*>(base + o_tiles);
-  a.nuc = reinterpret_cast<uint8_t*>(base + o_nuc);
-  a.pep = reinterpret_cast<uint8_t*>(base + o_pep);
+  a.nuc = static_cast<uint8_t*>(p->out_arena);
+  a.pep = static_cast<uint8_t*>(p->out_arena) + ((out_nuc + 255) & ~255ull);
   a.total_nuc = B;
   a.total_pep = P;
   a.n_tiles = n_tiles;
@@ -1347,6 +1490,7 @@ void magot_plan_destroy(magot_plan* p) {
   if (!p) return;
   if (p->ctx) (void)hipSetDevice(p->ctx->device);
   if (p->arena) (void)hipFree(p->arena);
+  if (p->out_arena) (void)hipFree(p->out_arena);
   delete p;
 }
 

@@ -29,6 +29,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <sys/mman.h>
+
 #include "common.h"
 
 namespace magot {
@@ -592,6 +594,41 @@ struct LineParser {
   }
 };
 
+// Pages of freshly reserved buffers mapped ahead of their first writes,
+// madvise(MADV_POPULATE_WRITE) over page-aligned pieces on several threads
+// (the kernel zeroes the pages without a fault per page).  Best effort: a
+// kernel without it leaves the pages to fault in on use.
+struct Prefault {
+  struct Range {
+    uintptr_t a, b;
+  };
+  std::vector<Range> ranges;
+  void add(const void* p, size_t bytes) {
+    const uintptr_t pg = 4096;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + pg - 1) & ~(pg - 1);
+    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(pg - 1);
+    for (uintptr_t x = a; x < b; x += (8u << 20)) ranges.push_back({x, std::min(b, x + (8u << 20))});
+  }
+  void run(unsigned threads) {
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < ranges.size();)
+        (void)madvise(reinterpret_cast<void*>(ranges[i].a), ranges[i].b - ranges[i].a,
+                      kMadvPopulateWrite);
+    };
+    std::vector<std::thread> pool;
+    for (unsigned t = 1; t < std::min<size_t>(threads, ranges.size()); ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+  }
+  size_t bytes() const {
+    size_t n = 0;
+    for (const Range& r : ranges) n += r.b - r.a;
+    return n;
+  }
+  static constexpr int kMadvPopulateWrite = 23;  // MADV_POPULATE_WRITE (Linux 5.14)
+};
+
 // read_gff in two passes: the per-line work (columns, tags, IDs, hashes) in
 // parallel over newline-aligned chunks of the text, then the model updates
 // (de-duplication, tables, parents) in file order.  Any diagnostic path
@@ -683,10 +720,28 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
   M.id_types.reserve(total + 16);
   M.first_table.reserve(total + 16);
   M.first_feat.reserve(total + 16);
-
+  M.ids.strs.reserve(total + 16);
   // model updates in file order
   std::vector<uint32_t> renamed;  // per ID: 0, or the last suffix used
   renamed.reserve(total + 16);
+  {
+    // the ordered pass below writes these in growing order; their pages are
+    // mapped here, on every host thread at once (C3: ~0.5 GB that the pass
+    // would otherwise fault in one page at a time)
+    Prefault pf;
+    pf.add(&M.ids.slots[0], M.ids.slots.size() * 8);
+    pf.add(M.ids.strs.data(), M.ids.strs.capacity() * sizeof(sv));
+    pf.add(M.feats.data(), M.feats.capacity() * sizeof(Feature));
+    pf.add(M.id_types.data(), M.id_types.capacity() * 8);
+    pf.add(M.first_table.data(), M.first_table.capacity());
+    pf.add(M.first_feat.data(), M.first_feat.capacity() * 4);
+    pf.add(renamed.data(), renamed.capacity() * 4);
+    pf.run(hw);
+    if (std::getenv("MAGOT_GFF_TIMING"))
+      fprintf(stderr, "[gffplan] prefault  %.3f s (%zu MiB)\n",
+              std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(),
+              pf.bytes() >> 20);
+  }
   std::string nid;
   std::vector<uint32_t> hier_table;
   for (const std::string& hk : F.hierarchy)
@@ -876,6 +931,7 @@ struct Lowered {
 struct magot_gffplan : magot::Lowered {
   magot::Model model;
   bool protein = false;
+  int stage = 0;  // 1: read (magot_gff_read), 2: lowered (magot_gff_lower)
 };
 
 namespace magot {
@@ -1139,30 +1195,60 @@ using magot::Unsupported;
 
 extern "C" {
 
-int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
-                   const uint64_t* contig_lens, uint32_t n_contigs, const char* feature,
-                   uint32_t flags, magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx) {
-  if (!out || (gff_len && !gff) || (n_contigs && (!seqids || !contig_lens)) || !feature) {
-    magot::set_error("magot_gff_plan: null argument");
+namespace {
+// MAGOT_GFF_TIMING: per-phase wall times on stderr
+struct GffLap {
+  const bool on = std::getenv("MAGOT_GFF_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  void operator()(const char* what) {
+    if (!on) return;
+    const auto t1 = std::chrono::steady_clock::now();
+    fprintf(stderr, "[gffplan] %-10s %.3f s\n", what,
+            std::chrono::duration<double>(t1 - t0).count());
+    t0 = t1;
+  }
+};
+}  // namespace
+
+int magot_gff_read(const char* gff, uint64_t gff_len, uint32_t flags, magot_gffplan** out) {
+  if (!out || (gff_len && !gff)) {
+    magot::set_error("magot_gff_read: null argument");
     return MAGOT_ERR_ARG;
   }
   *out = nullptr;
   std::unique_ptr<magot_gffplan> P(new magot_gffplan());
-  const bool genomic = (flags & MAGOT_GFF_GENOMIC) != 0;
-  P->protein = (flags & MAGOT_GFF_PROTEIN) != 0 && !genomic;  // genomic: never translated
-  const bool timing = std::getenv("MAGOT_GFF_TIMING") != nullptr;
-  auto now = [] { return std::chrono::steady_clock::now(); };
-  auto t0 = now();
-  auto lap = [&](const char* what) {
-    if (!timing) return;
-    const auto t1 = now();
-    fprintf(stderr, "[gffplan] %-10s %.3f s\n", what,
-            std::chrono::duration<double>(t1 - t0).count());
-    t0 = t1;
-  };
+  GffLap lap;
   try {
     magot::read_gff(P->model, gff, gff_len, (flags & MAGOT_GFF_FROM_EXONS) != 0);
     lap("read_gff");
+  } catch (const Unsupported&) {
+    magot::set_error("magot_gff_read: input takes a diagnostic path; use the object path");
+    return MAGOT_ERR_UNSUPPORTED;
+  } catch (const std::exception& e) {
+    magot::set_error(std::string("magot_gff_read: ") + e.what());
+    return MAGOT_ERR_ARG;
+  }
+  P->stage = 1;
+  *out = P.release();
+  return MAGOT_OK;
+}
+
+int magot_gff_lower(magot_gffplan* P, const char* const* seqids, const uint64_t* contig_lens,
+                    uint32_t n_contigs, const char* feature, uint32_t flags, uint64_t* n_exons,
+                    uint64_t* n_tx) {
+  if (!P || (n_contigs && (!seqids || !contig_lens)) || !feature) {
+    magot::set_error("magot_gff_lower: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  if (P->stage != 1) {
+    magot::set_error("magot_gff_lower: plan not read (magot_gff_read) or already lowered");
+    return MAGOT_ERR_STATE;
+  }
+  P->stage = 2;
+  const bool genomic = (flags & MAGOT_GFF_GENOMIC) != 0;
+  P->protein = (flags & MAGOT_GFF_PROTEIN) != 0 && !genomic;  // genomic: never translated
+  GffLap lap;
+  try {
     magot::Model& M = P->model;
     std::unordered_map<std::string, uint32_t> contig_of;
     for (uint32_t i = 0; i < n_contigs; ++i) contig_of[seqids[i]] = i;  // last duplicate wins
@@ -1233,15 +1319,32 @@ int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
     }
     lap("lower");
   } catch (const Unsupported&) {
-    magot::set_error("magot_gff_plan: input takes a diagnostic path; use the object path");
+    magot::set_error("magot_gff_lower: input takes a diagnostic path; use the object path");
     return MAGOT_ERR_UNSUPPORTED;
   } catch (const std::exception& e) {
-    magot::set_error(std::string("magot_gff_plan: ") + e.what());
+    magot::set_error(std::string("magot_gff_lower: ") + e.what());
     return MAGOT_ERR_ARG;
   }
   if (n_exons) *n_exons = P->exons.size();
   if (n_tx) *n_tx = P->txs.size();
-  *out = P.release();
+  return MAGOT_OK;
+}
+
+int magot_gff_plan(const char* gff, uint64_t gff_len, const char* const* seqids,
+                   const uint64_t* contig_lens, uint32_t n_contigs, const char* feature,
+                   uint32_t flags, magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx) {
+  if (!out || (gff_len && !gff) || (n_contigs && (!seqids || !contig_lens)) || !feature) {
+    magot::set_error("magot_gff_plan: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *out = nullptr;
+  magot_gffplan* P = nullptr;
+  if (int rc = magot_gff_read(gff, gff_len, flags, &P)) return rc;
+  if (int rc = magot_gff_lower(P, seqids, contig_lens, n_contigs, feature, flags, n_exons, n_tx)) {
+    magot_gffplan_destroy(P);
+    return rc;
+  }
+  *out = P;
   return MAGOT_OK;
 }
 

@@ -580,6 +580,13 @@ class GffPlan(object):
         check(rc, 'magot_gff_plan')
         return cls(h, ne.value, nt.value, protein and not genomic)
 
+    @staticmethod
+    def flags(protein=False, order='insertion', longest=False, genomic=False, from_exons=False):
+        return (_lib.GFF_PROTEIN if protein else 0) | \
+            (_lib.GFF_ORDER_PY2 if order == 'py2' else 0) | \
+            (_lib.GFF_LONGEST if longest else 0) | (_lib.GFF_GENOMIC if genomic else 0) | \
+            (_lib.GFF_FROM_EXONS if from_exons else 0)
+
     @classmethod
     def flank(cls, gff, names, lengths, sequence_length, stream, feature_type='gene',
               namefrom='ID'):
@@ -620,6 +627,71 @@ class GffPlan(object):
         if self.handle:
             _lib.lib().magot_gffplan_destroy(self.handle)
             self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class GffRead(object):
+    """read_gff done natively (magot_gff_read) before the genome's contigs are
+    known; ``lower`` turns it into a GffPlan against them (magot_gff_lower).
+    gff2fasta reads the GFF this way while another thread loads the FASTA.
+    ``read`` returns None when the input takes a diagnostic path."""
+
+    def __init__(self, handle, text, from_exons):
+        self.handle = handle
+        self._text = text  # the plan reads views of it until lower() returns
+        self.from_exons = from_exons
+
+    @classmethod
+    def read(cls, gff, from_exons=False):
+        L = _lib.lib()
+        text = _text_view(gff)
+        h = ctypes.c_void_p()
+        rc = L.magot_gff_read(_text_ptr(text), len(text),
+                              GffPlan.flags(from_exons=from_exons), ctypes.byref(h))
+        if rc == _lib.ERR_UNSUPPORTED:
+            if h.value:
+                L.magot_gffplan_destroy(h)
+            return None
+        check(rc, 'magot_gff_read')
+        return cls(h, text, from_exons)
+
+    def lower(self, names, lengths, feature='gene', protein=False, order='insertion',
+              longest=False, genomic=False):
+        """The GffPlan (this object gives its handle up), or None when the
+        lowering takes a diagnostic path (the handle is freed)."""
+        if not self.handle:
+            raise MagotError('GffRead.lower: already lowered or closed')
+        L = _lib.lib()
+        n = len(names)
+        arr = (ctypes.c_char_p * max(n, 1))(*[_as_bytes(x) for x in names])
+        lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint64))
+        flags = GffPlan.flags(protein, order, longest, genomic, self.from_exons)
+        ne, nt = ctypes.c_uint64(), ctypes.c_uint64()
+        h, self.handle = self.handle, None
+        try:
+            rc = L.magot_gff_lower(h, arr, lens.ctypes.data_as(_lib._u64p), n, _as_bytes(feature),
+                                   flags, ctypes.byref(ne), ctypes.byref(nt))
+            if rc == _lib.ERR_UNSUPPORTED:
+                return None
+            check(rc, 'magot_gff_lower')
+            plan = GffPlan(h, ne.value, nt.value, protein and not genomic)
+            h = None
+            return plan
+        finally:
+            self._text = None
+            if h is not None:
+                L.magot_gffplan_destroy(h)
+
+    def close(self):
+        if self.handle:
+            _lib.lib().magot_gffplan_destroy(self.handle)
+            self.handle = None
+        self._text = None
 
     def __del__(self):
         try:

@@ -44,6 +44,7 @@ class _Clock(object):
         self.on = os.environ.get('MAGOT_CLI_TIMING') == '1'
         self.t0 = self.last = time.perf_counter()
         self.laps, self.stamps = {}, {}
+        self.release_thread = None
 
     def lap(self, name):
         if self.on:
@@ -60,6 +61,33 @@ class _Clock(object):
             sys.stderr.write(json.dumps({'cli_phases_s': self.laps, 'cli_stamps_s': self.stamps,
                                          'cli_total_s': time.perf_counter() - self.t0}) + '\n')
             sys.stderr.flush()
+
+
+class _Release(object):
+    """What one CLI call closes when it is done, in order.  ``later()``
+    closes it on a background thread and returns that thread: once the
+    text is in the caller's hands, freeing the device buffers and the
+    planner's host tables (C3: ~0.12 s) need not delay it.  The thread is
+    not a daemon, so an interpreter that exits first still waits for it."""
+
+    def __init__(self):
+        self.objs = []
+
+    def add(self, obj):
+        if obj is not None:
+            self.objs.append(obj)
+        return obj
+
+    def now(self):
+        objs, self.objs = self.objs, []
+        for obj in objs:
+            obj.close()
+
+    def later(self):
+        import threading
+        th = threading.Thread(target=self.now, name='magot-release')
+        th.start()
+        return th
 
 
 def _literal(text):
@@ -134,15 +162,10 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
     protein = seq_type == 'protein'
     clock = clock or _Clock()
 
-    def plan_gff(names, lengths):
-        return engine.GffPlan.build(genome.read_buffer(gff), names, lengths, protein=protein,
-                                    order=order, longest=longest, genomic=genomic,
-                                    from_exons=from_exons)
-
-    # the FASTA is read and packed natively; Python reader for unusual headers.
-    # The GFF needs only the contig names and lengths (a host scan of the
-    # FASTA), so it is planned while another thread starts the device and
-    # uploads and packs the genome (both native calls release the GIL).
+    # The FASTA is read and packed natively (Python reader for unusual
+    # headers) on another thread, which starts the device first; this thread
+    # reads the GFF meanwhile (read_gff needs no genome), then lowers it
+    # against the loaded genome's contigs.  Both native calls release the GIL.
     from concurrent.futures import ThreadPoolExecutor
     fa = genome.read_buffer(genome_sequence)
     clock.lap('fasta_map')
@@ -158,13 +181,9 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
 
     with ThreadPoolExecutor(1) as pool:
         loading = pool.submit(load, fa)
-        plan = None
         try:
-            index = engine.fasta_contigs(fa)  # the same reader as the load
-            clock.lap('fasta_index')
-            if index is not None:
-                plan = plan_gff(*index)
-                clock.lap('gff_read_and_plan')
+            read = engine.GffRead.read(genome.read_buffer(gff), from_exons=from_exons)
+            clock.lap('gff_read')
         except BaseException:
             # the genome may already be on the device: free it before raising
             try:
@@ -177,25 +196,38 @@ def _gff2fasta_native(genome_sequence, gff, seq_type, order, longest=False, geno
         try:
             dev = loading.result()
         except BaseException:
-            if plan is not None:
-                plan.close()
+            if read is not None:
+                read.close()
             raise
         clock.lap('wait_genome')
     owned = dev  # the FastaGenome this call loaded (closed on every return)
-    if dev is None and plan is not None:  # above one device plane
-        plan.close()
-        plan = None
-    elif dev is not None and plan is None:
-        dev.close()
+    if read is None:  # read_gff takes a diagnostic path: the object path
+        if dev is not None:
+            dev.close()
         return None, None
+
+    def plan_gff(names, lengths):
+        # lowers the one read (None when the lowering takes a diagnostic path)
+        return read.lower(names, lengths, protein=protein, order=order, longest=longest,
+                          genomic=genomic)
+
+    release = _Release()
     try:
-        return _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock)
+        plan = None
+        if dev is not None:
+            plan = plan_gff(dev.names, dev.lengths)
+            clock.lap('gff_lower')
+            if plan is None:
+                return None, None
+        return _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock, release)
     finally:
-        if owned is not None:
-            owned.close()
+        release.add(read)
+        release.add(owned)
+        clock.release_thread = release.later()
+        clock.lap('close')
 
 
-def _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock):
+def _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock, release):
     seqs = None
     if dev is None:
         seqs = genome.GenomeSequence(genome_sequence)
@@ -208,11 +240,14 @@ def _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock):
         if plan is None:
             return None, seqs
     try:
-        # record order: the CLI launches once, so the genome-order layout's
-        # ~12 us off the kernel would cost ~60 ms more planning on the host
-        # (profiles/r05/text_assembly/)
+        # records laid out in genome order on the device (neighbouring loci in
+        # neighbouring tiles share genome lines: the kernel the bench line
+        # times); the device text assembly reads each record at its place, so
+        # the text is the record-order text.  longest=True over peptides
+        # fetches the payloads for a host render: record order there.
+        out = engine.OUT_PEP if plan.protein else engine.OUT_NUC
         ex = engine.ExtractionPlan(dev, plan.exons, plan.txs,
-                                   engine.OUT_PEP if plan.protein else engine.OUT_NUC)
+                                   out if plan.n_select else out | engine.OUT_GENOME_ORDER)
         clock.lap('plan_create')
         if plan.n_select:
             # longest=True over peptides: the render picks from the trimmed
@@ -232,10 +267,10 @@ def _gff2fasta_run(genome_sequence, dev, plan, plan_gff, clock):
             clock.lap('text_d2h')
             return out, None
         finally:
-            text.close()
-            ex.close()
+            release.add(text)
+            release.add(ex)
     finally:
-        plan.close()
+        release.add(plan)
 
 
 def _cds_translate(seq, seg_off):

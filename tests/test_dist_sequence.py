@@ -175,8 +175,9 @@ def test_dist_setup_binds_device_before_the_group(monkeypatch, tmp_path):
     monkeypatch.setattr(bench, 'bind_device', fake_bind)
     monkeypatch.delenv('MAGOT_DIST_BACKEND', raising=False)
     monkeypatch.setenv('TMPDIR', str(tmp_path))
-    for k in ('NCCL_DEBUG', 'NCCL_DEBUG_SUBSYS', 'NCCL_DEBUG_FILE'):
+    for k in ('NCCL_DEBUG_SUBSYS', 'NCCL_DEBUG_FILE'):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv('NCCL_DEBUG', 'VERSION')      # the pool's boxes preset it
     seen = []
 
     def fake_init(**kw):

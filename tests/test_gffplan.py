@@ -388,3 +388,62 @@ def test_native_plan_many_contigs(fmt):
         got = native_gff2fasta(fasta, gff, seq_type, 'py2')
         assert got is not None
         assert got == mo.gff2fasta(fasta, gff, seq_type=seq_type, order='py2')
+
+
+def _tables_text(plan, seqs):
+    return (plan.exons.tobytes(), plan.txs.tobytes(), plan.render(*_payloads(plan, seqs)))
+
+
+@pytest.mark.parametrize('fmt', ['gff3', 'gtf'])
+@pytest.mark.parametrize('kw', [{}, {'protein': True, 'order': 'py2'},
+                                {'genomic': True}, {'protein': True, 'longest': True}])
+def test_two_step_read_then_lower_equals_one_call(fmt, kw):
+    """gff2fasta reads the GFF (magot_gff_read) while the genome loads and
+    lowers it against the loaded contigs afterwards (magot_gff_lower): the
+    same tables and text as magot_gff_plan in one call."""
+    w = synth.make('small', seed=23, genome_bases=300_000, n_tx=200, iupac_rate=1e-3)
+    gs = G.GenomeSequence(w.fasta_text())
+    names = list(gs)
+    lens = [len(gs[n]) for n in names]
+    gff = w.gff3_text() if fmt == 'gff3' else w.gtf_text()
+    one = engine.GffPlan.build(gff, names, lens, **kw)
+    rd = engine.GffRead.read(gff)
+    two = rd.lower(names, lens, **kw)
+    assert rd.handle is None                      # the plan took the handle over
+    seqs = [gs[n] for n in names]
+    assert _tables_text(one, seqs) == _tables_text(two, seqs)
+    assert (one.protein, one.n_select) == (two.protein, two.n_select)
+    one.close()
+    two.close()
+    with pytest.raises(engine.MagotError):        # one lowering per read
+        rd.lower(names, lens)
+
+
+def test_two_step_declines_like_one_call():
+    gs = G.GenomeSequence('>c1\nACGTACGTACGT\n')
+    # read_gff itself declines (orphan parent) ...
+    assert engine.GffRead.read('c1\tx\tCDS\t1\t9\t.\t+\t0\tID=c1;Parent=nope\n') is None
+    # ... or only the lowering does (a seqid the genome lacks)
+    rd = engine.GffRead.read('zz\tx\tgene\t1\t9\t.\t+\t.\tID=g1\nzz\tx\tmRNA\t1\t9\t.\t+\t.\t'
+                             'ID=m1;Parent=g1\nzz\tx\tCDS\t1\t9\t.\t+\t0\tID=c1;Parent=m1\n')
+    assert rd is not None
+    assert rd.lower(list(gs), [12], protein=True) is None
+    assert rd.handle is None
+
+
+def test_two_step_abi_state_errors():
+    import ctypes
+    from magot_amd import _lib
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    text = b'c1\tx\tgene\t1\t9\t.\t+\t.\tID=g1\n'
+    assert L.magot_gff_read(text, len(text), 0, ctypes.byref(h)) == 0
+    names = (ctypes.c_char_p * 1)(b'c1')
+    lens = np.array([12], dtype=np.uint64)
+    ne, nt = ctypes.c_uint64(), ctypes.c_uint64()
+    args = (names, lens.ctypes.data_as(_lib._u64p), 1, b'gene', 0, ctypes.byref(ne),
+            ctypes.byref(nt))
+    assert L.magot_gff_lower(h, *args) == 0
+    assert L.magot_gff_lower(h, *args) == _lib.ERR_STATE      # lowered already
+    L.magot_gffplan_destroy(h)
+    assert L.magot_gff_lower(None, *args) == _lib.ERR_ARG
