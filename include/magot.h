@@ -484,6 +484,10 @@ int magot_flank_plan(const char* gff, uint64_t gff_len, const char* const* seqid
                      magot_gffplan** out, uint64_t* n_exons, uint64_t* n_tx);
 /* Copy the planned tables (n_exons / n_tx entries from magot_gff_plan). */
 int magot_gffplan_tables(const magot_gffplan* p, magot_exon* exons, magot_tx* txs);
+/* The planned tables in place (n_exons / n_tx rows, valid until the plan is
+ * destroyed; NULL when empty): magot_plan_create reads them without a copy. */
+int magot_gffplan_table_views(const magot_gffplan* p, const magot_exon** exons,
+                              const magot_tx** txs);
 /* The FASTA text: skeleton + record payloads from magot_plan_fetch (nuc for
  * nucleotide plans, untrimmed pep for protein; the leading-'X' trim of
  * genome.py:819-821 is applied here).  out == NULL: *out_len = size only. */

@@ -35,7 +35,8 @@ EXPORTS = (
     'magot_revcomp_batch', 'magot_translate_sizes', 'magot_translate_batch',
     'magot_codon_symbols', 'magot_revcomp', 'magot_translate',
     'magot_gff_plan', 'magot_gff_read', 'magot_gff_lower', 'magot_flank_plan',
-    'magot_gffplan_tables', 'magot_gffplan_render', 'magot_gffplan_destroy',
+    'magot_gffplan_tables', 'magot_gffplan_table_views', 'magot_gffplan_render',
+    'magot_gffplan_destroy',
     'magot_gffplan_selections', 'magot_cds_scan', 'magot_cds_render',
     'magot_genome_export', 'magot_genome_copy_arena', 'magot_genome_attach',
     'magot_plan_copy_outputs',
@@ -128,6 +129,8 @@ def _declare(lib):
                                             ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(_vp),
                                             _u64p, _u64p]),
         'magot_gffplan_tables': (ctypes.c_int, [_vp, _vp, _vp]),
+        'magot_gffplan_table_views': (ctypes.c_int, [_vp, ctypes.POINTER(_vp),
+                                                     ctypes.POINTER(_vp)]),
         'magot_gffplan_render': (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
                                                 _u64p]),
         'magot_gffplan_destroy': (None, [_vp]),

@@ -882,7 +882,11 @@ std::vector<uint32_t> py2_dict_order(const std::vector<uint32_t>& keys,
       perturb >>= 5;
     }
   };
-  for (uint32_t k : keys) {
+  constexpr size_t kAhead = 8;  // the slot a key probes first, fetched a few keys ahead
+  for (size_t q = 0; q < keys.size(); ++q) {
+    if (q + kAhead < keys.size())
+      __builtin_prefetch(&slots[hash[keys[q + kAhead]] & (slots.size() - 1)]);
+    const uint32_t k = keys[q];
     if (!place(slots, k)) continue;
     ++used;
     if (used * 3 >= slots.size() * 2) {
@@ -1260,15 +1264,26 @@ int magot_gff_lower(magot_gffplan* P, const char* const* seqids, const uint64_t*
     std::vector<uint32_t> id_of_feat(M.feats.size(), 0);
     for (uint32_t ti2 = 0; ti2 < M.tables.size(); ++ti2)
       for (uint32_t k : M.tables[ti2].keys) id_of_feat[(size_t)M.slot(ti2, k)] = k;
+    lap("feat_ids");
     auto ti = M.table_index.find(feature);
     if (ti == M.table_index.end()) throw Unsupported();  // AttributeError
     const magot::Table& T = M.tables[ti->second];
     std::vector<uint32_t> keys = T.keys;
     if (flags & MAGOT_GFF_ORDER_PY2) {
-      std::vector<uint64_t> hash(M.ids.strs.size());
-      for (uint32_t k : keys) hash[k] = magot::py2_hash(M.ids.strs[k]);
-      keys = magot::py2_dict_order(keys, hash);  // the table as built ...
-      keys = magot::py2_dict_order(keys, hash);  // ... and as deep-copied (genome.py:415)
+      // the dict simulation runs on positions in `keys` (hash per position:
+      // no table sized for every ID of the model)
+      std::vector<uint64_t> hash(keys.size());
+      std::vector<uint32_t> pos(keys.size());
+      for (size_t i = 0; i < keys.size(); ++i) {
+        hash[i] = magot::py2_hash(M.ids.strs[keys[i]]);
+        pos[i] = (uint32_t)i;
+      }
+      lap("py2_hash");
+      pos = magot::py2_dict_order(pos, hash);  // the table as built ...
+      pos = magot::py2_dict_order(pos, hash);  // ... and as deep-copied (genome.py:415)
+      std::vector<uint32_t> ordered(pos.size());
+      for (size_t i = 0; i < pos.size(); ++i) ordered[i] = keys[pos[i]];
+      keys.swap(ordered);
     }
     lap("order");
     // "\n".join(obj.get_fasta() for obj in table.values()): every object adds
@@ -1533,6 +1548,17 @@ int magot_flank_plan(const char* gff, uint64_t gff_len, const char* const* seqid
   if (n_exons) *n_exons = P->exons.size();
   if (n_tx) *n_tx = P->txs.size();
   *out = P.release();
+  return MAGOT_OK;
+}
+
+int magot_gffplan_table_views(const magot_gffplan* p, const magot_exon** exons,
+                              const magot_tx** txs) {
+  if (!p || !exons || !txs) {
+    magot::set_error("magot_gffplan_table_views: null argument");
+    return MAGOT_ERR_ARG;
+  }
+  *exons = p->exons.empty() ? nullptr : p->exons.data();
+  *txs = p->txs.empty() ? nullptr : p->txs.data();
   return MAGOT_OK;
 }
 

@@ -543,10 +543,14 @@ class GffPlan(object):
     def __init__(self, handle, n_exons, n_tx, protein):
         self.handle = handle
         self.protein = protein
-        self.exons = np.zeros(n_exons, dtype=EXON_DTYPE)
-        self.txs = np.zeros(n_tx, dtype=TX_DTYPE)
-        check(_lib.lib().magot_gffplan_tables(handle, ptr(self.exons), ptr(self.txs)),
-              'magot_gffplan_tables')
+        # the plan's own tables, viewed in place (C3: 72 MB not copied);
+        # close() turns the views into copies before the plan goes
+        ep, tp = ctypes.c_void_p(), ctypes.c_void_p()
+        check(_lib.lib().magot_gffplan_table_views(handle, ctypes.byref(ep), ctypes.byref(tp)),
+              'magot_gffplan_table_views')
+        self.exons = _view(ep.value, n_exons, EXON_DTYPE)
+        self.txs = _view(tp.value, n_tx, TX_DTYPE)
+        self._views = True
         n = ctypes.c_uint64()
         check(_lib.lib().magot_gffplan_selections(handle, ctypes.byref(n)),
               'magot_gffplan_selections')
@@ -625,6 +629,11 @@ class GffPlan(object):
 
     def close(self):
         if self.handle:
+            if self._views:
+                # the views die with the plan: anyone still holding the
+                # attributes keeps valid copies
+                self.exons, self.txs = self.exons.copy(), self.txs.copy()
+                self._views = False
             _lib.lib().magot_gffplan_destroy(self.handle)
             self.handle = None
 
@@ -633,6 +642,15 @@ class GffPlan(object):
             self.close()
         except Exception:
             pass
+
+
+def _view(addr, n, dtype):
+    """n rows of `dtype` at host address `addr` (not owned; empty when n == 0)."""
+    dtype = np.dtype(dtype)
+    if not n:
+        return np.zeros(0, dtype=dtype)
+    buf = (ctypes.c_uint8 * (n * dtype.itemsize)).from_address(addr)
+    return np.frombuffer(buf, dtype=dtype, count=n)
 
 
 class GffRead(object):
