@@ -187,23 +187,78 @@ struct Model {
   std::unordered_map<std::string, uint32_t> table_index;
   std::vector<uint32_t> rank;      // table -> rank in sorted-name order
   std::vector<Feature> feats;
-  std::vector<std::vector<uint32_t>> kid_lists;  // child IDs (ids) per parent feature
+  // Child IDs (ids) per parent feature.  The ordered pass appends them as
+  // chains through one pair of link arrays (no allocation per list: C3 has a
+  // million parents); flatten() then lays every list out contiguously
+  // (kid_off / kid_flat), which is what children() reads.
+  std::vector<uint32_t> kid_head, kid_tail, kid_n;  // per list
+  std::vector<uint32_t> link_child, link_next;      // per appended child
+  std::vector<uint64_t> kid_off;                    // per list + 1, after flatten()
+  std::vector<uint32_t> kid_flat;
 
   Model() {
     // AnnotationSet.__init__ (genome.py:528-533) creates these dicts
     for (const char* t : {"gene", "transcript", "CDS", "UTR"}) table(t);
   }
 
-  const std::vector<uint32_t>& children(const Feature& f) const {
-    static const std::vector<uint32_t> none;
-    return f.kids == ~0u ? none : kid_lists[f.kids];
+  struct Kids {
+    const uint32_t* p;
+    size_t n;
+    const uint32_t* begin() const { return p; }
+    const uint32_t* end() const { return p + n; }
+    bool empty() const { return n == 0; }
+    uint32_t operator[](size_t i) const { return p[i]; }
+  };
+  Kids children(const Feature& f) const {
+    if (f.kids == ~0u) return Kids{nullptr, 0};
+    return Kids{kid_flat.data() + kid_off[f.kids], (size_t)(kid_off[f.kids + 1] - kid_off[f.kids])};
   }
-  std::vector<uint32_t>& children_mut(Feature& f) {
+  bool has_child(const Feature& f, uint32_t child) const {
+    if (f.kids == ~0u) return false;
+    for (uint32_t k = kid_head[f.kids]; k != ~0u; k = link_next[k])
+      if (link_child[k] == child) return true;
+    return false;
+  }
+  void add_child(Feature& f, uint32_t child) {
+    const uint32_t k = (uint32_t)link_child.size();
+    link_child.push_back(child);
+    link_next.push_back(~0u);
     if (f.kids == ~0u) {
-      f.kids = (uint32_t)kid_lists.size();
-      kid_lists.emplace_back();
+      f.kids = (uint32_t)kid_head.size();
+      kid_head.push_back(k);
+      kid_tail.push_back(k);
+      kid_n.push_back(1);
+      return;
     }
-    return kid_lists[f.kids];
+    link_next[kid_tail[f.kids]] = k;
+    kid_tail[f.kids] = k;
+    ++kid_n[f.kids];
+  }
+  // the chains laid out as one array per list, in append order
+  void flatten(unsigned threads) {
+    const size_t nl = kid_head.size();
+    kid_off.assign(nl + 1, 0);
+    for (size_t l = 0; l < nl; ++l) kid_off[l + 1] = kid_off[l] + kid_n[l];
+    kid_flat.resize(link_child.size());
+    std::atomic<size_t> next{0};
+    const size_t step = 1 << 14;
+    auto work = [&]() {
+      for (size_t b; (b = next.fetch_add(step)) < nl;)
+        for (size_t l = b; l < std::min(nl, b + step); ++l) {
+          uint64_t o = kid_off[l];
+          for (uint32_t k = kid_head[l]; k != ~0u; k = link_next[k]) kid_flat[o++] = link_child[k];
+        }
+    };
+    std::vector<std::thread> pool;
+    const size_t nt = nl < 4 * step ? 1 : std::min<size_t>(threads, nl / step);
+    for (size_t t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto& t : pool) t.join();
+    std::vector<uint32_t>().swap(link_child);
+    std::vector<uint32_t>().swap(link_next);
+    std::vector<uint32_t>().swap(kid_head);
+    std::vector<uint32_t>().swap(kid_tail);
+    std::vector<uint32_t>().swap(kid_n);
   }
 
   uint32_t id(sv s) { return id(s, hash_sv(s)); }
@@ -721,6 +776,8 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
   M.first_table.reserve(total + 16);
   M.first_feat.reserve(total + 16);
   M.ids.strs.reserve(total + 16);
+  M.link_child.reserve(total + 16);  // one child per line with a parent (GFF3)
+  M.link_next.reserve(total + 16);
   // model updates in file order
   std::vector<uint32_t> renamed;  // per ID: 0, or the last suffix used
   renamed.reserve(total + 16);
@@ -736,6 +793,8 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
     pf.add(M.first_table.data(), M.first_table.capacity());
     pf.add(M.first_feat.data(), M.first_feat.capacity() * 4);
     pf.add(renamed.data(), renamed.capacity() * 4);
+    pf.add(M.link_child.data(), M.link_child.capacity() * 4);
+    pf.add(M.link_next.data(), M.link_next.capacity() * 4);
     pf.run(hw);
     if (std::getenv("MAGOT_GFF_TIMING"))
       fprintf(stderr, "[gffplan] prefault  %.3f s (%zu MiB)\n",
@@ -803,15 +862,15 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
           const uint32_t pk = M.id(HV[li].hv[level], HV[li].h_hv[level]);
           const int64_t have = M.slot(t, pk);
           if (have >= 0) {
-            auto& ch = M.children_mut(M.feats[(size_t)have]);
-            if (std::find(ch.begin(), ch.end(), child) == ch.end()) ch.push_back(child);
+            Feature& hf = M.feats[(size_t)have];
+            if (!M.has_child(hf, child)) M.add_child(hf, child);
           } else {
             Feature f;
             f.type = t;
             f.seqid = sq;
             f.strand = st;
             f.base = false;
-            M.children_mut(f).push_back(child);
+            M.add_child(f, child);
             M.feats.push_back(std::move(f));
             M.put(t, pk, (uint32_t)M.feats.size() - 1);
           }
@@ -827,10 +886,8 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
         Feature& holder = M.feats[(size_t)h];
         if (holder.base) throw Unsupported();  // BaseAnnotation has no child_list
         // without a hierarchy, a name interned on this line is in no child list yet
-        std::vector<uint32_t>& kids = M.children_mut(holder);
-        if ((idk >= n_ids && F.hierarchy.empty()) ||
-            std::find(kids.begin(), kids.end(), idk) == kids.end())
-          kids.push_back(idk);
+        if ((idk >= n_ids && F.hierarchy.empty()) || !M.has_child(holder, idk))
+          M.add_child(holder, idk);
       }
       if (ty_of[L.ftype] == ~0u) {  // the table is created at the type's first line
         const sv ft = P.ftypes.strs[L.ftype];
@@ -849,6 +906,10 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
       M.put(ty, idk, (uint32_t)M.feats.size() - 1);
     }
   }
+  if (std::getenv("MAGOT_GFF_TIMING"))
+    fprintf(stderr, "[gffplan] ordered  %.3f s\n",
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
+  M.flatten(hw);
 }
 
 // ---------------------------------------------------------------------------

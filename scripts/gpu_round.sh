@@ -110,6 +110,23 @@ if has e2e; then
   cat $OUT/e2e_protein.json
   rm -rf /tmp/magot_e2e
 fi
+if has gffab; then
+  # host planner A/B on the box's CPUs (binaries from scripts/gffplan_ab.sh build)
+  AB_TIMING=1 timeout -k 10 600 bash scripts/gffplan_ab.sh run $OUT/gffab 4 > $OUT/gffab.log 2>&1 || { tail -20 $OUT/gffab.log; exit 1; }
+  grep plan_s $OUT/gffab/gffplan_ab.txt
+fi
+if has whole; then
+  # the phase run (writes the C3 files and the reference out.fa; genome-order
+  # plan as the CLI builds it), then three whole gff2fasta calls on those
+  # files in fresh processes (the CLI's phase clock)
+  MAGOT_GFF_TIMING=1 MAGOT_PLAN_TIMING=1 timeout -k 10 900 python scripts/e2e_cli.py --config C3 --seq-type protein --layout genome > $OUT/e2e_protein.json 2> $OUT/e2e.err || { tail -20 $OUT/e2e.err; exit 1; }
+  cat $OUT/e2e_protein.json
+  for i in 1 2 3; do
+    MAGOT_GFF_TIMING=1 timeout -k 10 300 python scripts/e2e_cli.py --config C3 --seq-type protein --whole > $OUT/e2e_whole$i.json 2> $OUT/e2e_whole$i.err || { tail -20 $OUT/e2e_whole$i.err; exit 1; }
+    cat $OUT/e2e_whole$i.json
+  done
+  rm -rf /tmp/magot_e2e
+fi
 if has multi; then
   # two ranks launched by bench itself, sharing the one card over gloo (the
   # C4 orchestration; the driver's 8-GPU node runs it over RCCL)

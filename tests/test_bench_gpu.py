@@ -76,6 +76,31 @@ def test_bench_spawns_two_ranks_strong(tensors):
     assert d['config']['parallelism'].startswith('contig-sharded x2')
 
 
+def test_bench_torchrun_two_ranks_strong():
+    """The driver's own launch (``python -m torch.distributed.run --nnodes=1
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P bench.py
+    --gpus 2``): the ranks join torchrun's agent store through bench's tcp://
+    URL; gloo with device tensors, both ranks on this card."""
+    sys.path.insert(0, ROOT)
+    import bench
+    env = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    env.update({'MAGOT_DIST_BACKEND': 'gloo', 'MAGOT_COLLECTIVE_TENSORS': 'cuda'})
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+                        '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+                        '--master-port', str(bench._free_port()),
+                        os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--config', 'small'] +
+                       COMMON, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, _failure(r)
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{')]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['scaling'] == 'strong'
+    assert d['parity'].startswith('bit-exact'), d['parity']
+    assert d['outputs_gather']['parity'].startswith('bit-exact'), d['outputs_gather']
+
+
 def test_bench_spawns_two_ranks_weak():
     d = _bench(['--gpus', '2', '--config', 'small', '--mode', 'weak'] + COMMON,
                {'MAGOT_DIST_BACKEND': 'gloo'})

@@ -140,6 +140,35 @@ def test_dist_setup_one_rank_forced_gloo(tmp_path):
     assert r.stdout.strip().splitlines()[-1] == 'gloo'
 
 
+def test_dist_setup_under_torchrun_two_ranks(tmp_path):
+    """The driver's launch exactly: ``python -m torch.distributed.run --nnodes=1
+    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P``.  Each rank's
+    bench.dist_setup joins the elastic agent's store through the explicit
+    tcp:// URL (TORCHELASTIC_USE_AGENT_STORE), then a reduction, the
+    per-rank value gather and a barrier run over gloo."""
+    import subprocess
+    probe = tmp_path / 'probe.py'
+    probe.write_text(
+        'import os, sys\nsys.path.insert(0, %r)\nimport bench\n'
+        'd, r, l, n = bench.dist_setup()\n'
+        'assert n == 2 and d.get_world_size() == 2 and d.get_rank() == r\n'
+        'assert os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"\n'
+        'assert bench.allreduce_sum(d, r + 1.0) == 3.0\n'
+        'assert bench.all_values(d, 10.0 * (r + 1)) == [10.0, 20.0]\n'
+        'bench.barrier(d)\n'
+        'print("rank%%d %%s ok" %% (r, d.get_backend()), flush=True)\n'
+        'd.destroy_process_group()\n' % ROOT)
+    env = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+                        '--nproc-per-node', '2', '--master-addr', '127.0.0.1',
+                        '--master-port', str(_free_port()), str(probe)],
+                       env=env, capture_output=True, text=True, timeout=180, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert 'rank0 gloo ok' in r.stdout and 'rank1 gloo ok' in r.stdout, r.stdout
+
+
 # ---------------------------------------------------------------------------
 # C4 (strong) orchestration: magot_amd/shard.py
 # ---------------------------------------------------------------------------
