@@ -187,14 +187,11 @@ struct Model {
   std::unordered_map<std::string, uint32_t> table_index;
   std::vector<uint32_t> rank;      // table -> rank in sorted-name order
   std::vector<Feature> feats;
-  // Child IDs (ids) per parent feature.  The ordered pass appends them as
-  // chains through one pair of link arrays (no allocation per list: C3 has a
-  // million parents); flatten() then lays every list out contiguously
-  // (kid_off / kid_flat), which is what children() reads.
-  std::vector<uint32_t> kid_head, kid_tail, kid_n;  // per list
-  std::vector<uint32_t> link_child, link_next;      // per appended child
-  std::vector<uint64_t> kid_off;                    // per list + 1, after flatten()
-  std::vector<uint32_t> kid_flat;
+  // Child IDs (ids) per parent feature, as chains through one pair of link
+  // arrays in append order (no allocation per list: C3 has a million
+  // parents); children() walks a chain.
+  std::vector<uint32_t> kid_head, kid_tail;     // per list
+  std::vector<uint32_t> link_child, link_next;  // per appended child
 
   Model() {
     // AnnotationSet.__init__ (genome.py:528-533) creates these dicts
@@ -202,21 +199,29 @@ struct Model {
   }
 
   struct Kids {
-    const uint32_t* p;
-    size_t n;
-    const uint32_t* begin() const { return p; }
-    const uint32_t* end() const { return p + n; }
-    bool empty() const { return n == 0; }
-    uint32_t operator[](size_t i) const { return p[i]; }
+    const Model* m;
+    uint32_t head;  // first link, ~0u: no children
+    struct It {
+      const Model* m;
+      uint32_t k;
+      uint32_t operator*() const { return m->link_child[k]; }
+      It& operator++() {
+        k = m->link_next[k];
+        return *this;
+      }
+      bool operator!=(const It& o) const { return k != o.k; }
+    };
+    It begin() const { return It{m, head}; }
+    It end() const { return It{m, ~0u}; }
+    bool empty() const { return head == ~0u; }
+    uint32_t front() const { return m->link_child[head]; }
   };
   Kids children(const Feature& f) const {
-    if (f.kids == ~0u) return Kids{nullptr, 0};
-    return Kids{kid_flat.data() + kid_off[f.kids], (size_t)(kid_off[f.kids + 1] - kid_off[f.kids])};
+    return Kids{this, f.kids == ~0u ? ~0u : kid_head[f.kids]};
   }
   bool has_child(const Feature& f, uint32_t child) const {
-    if (f.kids == ~0u) return false;
-    for (uint32_t k = kid_head[f.kids]; k != ~0u; k = link_next[k])
-      if (link_child[k] == child) return true;
+    for (uint32_t c : children(f))
+      if (c == child) return true;
     return false;
   }
   void add_child(Feature& f, uint32_t child) {
@@ -227,38 +232,10 @@ struct Model {
       f.kids = (uint32_t)kid_head.size();
       kid_head.push_back(k);
       kid_tail.push_back(k);
-      kid_n.push_back(1);
       return;
     }
     link_next[kid_tail[f.kids]] = k;
     kid_tail[f.kids] = k;
-    ++kid_n[f.kids];
-  }
-  // the chains laid out as one array per list, in append order
-  void flatten(unsigned threads) {
-    const size_t nl = kid_head.size();
-    kid_off.assign(nl + 1, 0);
-    for (size_t l = 0; l < nl; ++l) kid_off[l + 1] = kid_off[l] + kid_n[l];
-    kid_flat.resize(link_child.size());
-    std::atomic<size_t> next{0};
-    const size_t step = 1 << 14;
-    auto work = [&]() {
-      for (size_t b; (b = next.fetch_add(step)) < nl;)
-        for (size_t l = b; l < std::min(nl, b + step); ++l) {
-          uint64_t o = kid_off[l];
-          for (uint32_t k = kid_head[l]; k != ~0u; k = link_next[k]) kid_flat[o++] = link_child[k];
-        }
-    };
-    std::vector<std::thread> pool;
-    const size_t nt = nl < 4 * step ? 1 : std::min<size_t>(threads, nl / step);
-    for (size_t t = 1; t < nt; ++t) pool.emplace_back(work);
-    work();
-    for (auto& t : pool) t.join();
-    std::vector<uint32_t>().swap(link_child);
-    std::vector<uint32_t>().swap(link_next);
-    std::vector<uint32_t>().swap(kid_head);
-    std::vector<uint32_t>().swap(kid_tail);
-    std::vector<uint32_t>().swap(kid_n);
   }
 
   uint32_t id(sv s) { return id(s, hash_sv(s)); }
@@ -906,10 +883,6 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
       M.put(ty, idk, (uint32_t)M.feats.size() - 1);
     }
   }
-  if (std::getenv("MAGOT_GFF_TIMING"))
-    fprintf(stderr, "[gffplan] ordered  %.3f s\n",
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
-  M.flatten(hw);
 }
 
 // ---------------------------------------------------------------------------
@@ -1046,7 +1019,7 @@ struct Lowering {
   uint64_t fasta(uint32_t fi, bool first_in_join) {
     const Feature& F = M.feats[fi];
     if (M.children(F).empty()) return 0;
-    const int64_t first = M.lookup(M.children(F)[0]);
+    const int64_t first = M.lookup(M.children(F).front());
     if (first < 0) throw Unsupported();  // KeyError
     if (M.feats[(size_t)first].base) {
       // base branch: child_dict keyed by coords (last wins), order by the last

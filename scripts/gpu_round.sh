@@ -111,7 +111,9 @@ if has e2e; then
   rm -rf /tmp/magot_e2e
 fi
 if has gffab; then
-  # host planner A/B on the box's CPUs (binaries from scripts/gffplan_ab.sh build)
+  # host planner A/B on the box's CPUs: HEAD's gffplan.cpp against the copy
+  # under scripts/ab_old/ (git-ignored), both built here
+  bash scripts/gffplan_ab.sh build scripts/ab_old/magot_amd/csrc/gffplan.cpp > $OUT/gffab_build.log 2>&1 || { tail -20 $OUT/gffab_build.log; exit 1; }
   AB_TIMING=1 timeout -k 10 600 bash scripts/gffplan_ab.sh run $OUT/gffab 4 > $OUT/gffab.log 2>&1 || { tail -20 $OUT/gffab.log; exit 1; }
   grep plan_s $OUT/gffab/gffplan_ab.txt
 fi
