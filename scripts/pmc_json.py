@@ -45,6 +45,11 @@ def main(d, config, kernel):
                        'include Infinity Cache hits (an upper bound on HBM reads)',
     }
     path = os.path.join(ROOT, 'profiles', 'pmc_%s.json' % config)
+    if os.path.exists(path):  # keep an attribution made from the lines (scripts/c5_lines.py)
+        with open(path) as fh:
+            old = json.load(fh)
+        if 'read_split' in old:
+            out['read_split'] = old['read_split']
     with open(path, 'w') as fh:
         json.dump(out, fh, indent=1)
         fh.write('\n')
