@@ -661,402 +661,6 @@ struct Prefault {
   static constexpr int kMadvPopulateWrite = 23;  // MADV_POPULATE_WRITE (Linux 5.14)
 };
 
-// fn(i) for i in [0, n) on up to `threads` host threads (dynamic
-// assignment); the first exception any of them throws is rethrown here.
-template <class Fn>
-void parallel_for(size_t n, unsigned threads, Fn fn) {
-  FirstError failed;
-  std::atomic<size_t> next{0};
-  std::atomic<bool> stop{false};
-  auto work = [&]() {
-    for (size_t i; !stop.load(std::memory_order_relaxed) && (i = next.fetch_add(1)) < n;) {
-      try {
-        fn(i);
-      } catch (...) {
-        failed.set();
-        stop = true;
-      }
-    }
-  };
-  std::vector<std::thread> pool;
-  for (size_t t = 1; t < std::min<size_t>(threads, n); ++t) pool.emplace_back(work);
-  work();
-  for (auto& t : pool) t.join();
-  failed.rethrow();
-}
-
-// The file-order pass of read_gff (genome.py:320-398) for inputs without a
-// GTF hierarchy, on host threads.  Without a hierarchy every accepted line
-// interns exactly one new ID, its final key: the line's ID, or from the second
-// line holding that ID on, ID2, ID-3, ... (genome.py:330-338).  Whether a
-// line's ID is taken then depends only on the earlier lines holding the same
-// ID string -- unless some final key equals another (a generated name
-// meeting a literal one, which the reference does not re-check): then two
-// lines' final keys are equal, and the exact serial pass runs instead.  So:
-//  1. per ID string, in file order (lines partitioned by the ID's hash), the
-//     line's renaming count and its final key's hash;
-//  2. every final key distinct, else return false (the serial pass);
-//  3. a line's parent is the line whose final key it names, which must come
-//     earlier and not be a base feature (else the input declines, as the
-//     serial pass would: orphan / BaseAnnotation, genome.py:352-366);
-//  4. line i is feature i and ID i: the tables are filled at once.
-// Model::ids gets the strings but not its hash table (nothing looks IDs up
-// by name after read_gff).
-bool ordered_parallel(Model& M, const std::vector<std::vector<GffLine>>& lines,
-                      const std::vector<std::unique_ptr<LineParser>>& parsers, unsigned hw) {
-  const bool timing = std::getenv("MAGOT_GFF_TIMING") != nullptr;
-  auto t_last = std::chrono::steady_clock::now();
-  auto lap = [&](const char* what) {
-    if (!timing) return;
-    const auto t = std::chrono::steady_clock::now();
-    fprintf(stderr, "[gffplan]   %-16s %.3f s\n", what, std::chrono::duration<double>(t - t_last).count());
-    t_last = t;
-  };
-  const size_t nc = lines.size();
-  std::vector<uint64_t> base(nc + 1, 0);  // global index of each chunk's first line
-  for (size_t c = 0; c < nc; ++c) base[c + 1] = base[c] + lines[c].size();
-  const uint64_t n = base[nc];
-  if (n == 0 || n >= (1ull << 31)) return false;
-  constexpr int kPartBits = 8;
-  constexpr size_t kParts = size_t(1) << kPartBits;
-  auto part_of = [](uint64_t h) { return (size_t)(h >> (64 - kPartBits)); };
-  // a line's locator: chunk << 32 | index in the chunk
-  auto line_at = [&](uint64_t loc) -> const GffLine& { return lines[loc >> 32][(uint32_t)loc]; };
-  auto gidx = [&](uint64_t loc) { return base[loc >> 32] + (uint32_t)loc; };
-  auto locate = [&](uint64_t i) -> uint64_t {  // global index -> locator
-    const size_t c = (size_t)(std::upper_bound(base.begin(), base.end(), i) - base.begin()) - 1;
-    return ((uint64_t)c << 32) | (uint32_t)(i - base[c]);
-  };
-  std::vector<uint32_t> rep(n);  // per line: 0 its ID, j >= 1 the j-th renaming of it
-  std::vector<uint64_t> fkh(n);  // per line: hash of its final key
-  // the final key of a line, compared with a string without building it
-  auto suffix = [](uint32_t j, char* buf) -> sv {  // dup_name's suffix
-    char* e = buf + 16;
-    char* q = e;
-    if (j == 1) {
-      *--q = '2';
-    } else {
-      for (uint32_t v = j + 1; v; v /= 10) *--q = (char)('0' + v % 10);
-      *--q = '-';
-    }
-    return sv(q, (size_t)(e - q));
-  };
-  auto key_is = [&](uint64_t loc, sv s) {
-    const GffLine& L = line_at(loc);
-    const uint32_t j = rep[gidx(loc)];
-    if (j == 0) return L.id == s;
-    char b[16];
-    const sv x = suffix(j, b);
-    return s.size() == L.id.size() + x.size() && s.substr(0, L.id.size()) == L.id &&
-           s.substr(L.id.size()) == x;
-  };
-  auto key_of = [&](uint64_t loc, std::string& out) {
-    const GffLine& L = line_at(loc);
-    char b[16];
-    out.assign(L.id.data(), L.id.size());
-    if (const uint32_t j = rep[gidx(loc)]) out.append(suffix(j, b));
-  };
-  // line locators grouped by partition of a per-line hash, file order inside
-  std::vector<uint64_t> loc(n), off(kParts + 1), cnt(nc * kParts);
-  auto scatter = [&](auto hash_of) {
-    parallel_for(nc, hw, [&](size_t c) {
-      uint64_t* k = &cnt[c * kParts];
-      std::fill(k, k + kParts, 0);
-      for (size_t li = 0; li < lines[c].size(); ++li) ++k[part_of(hash_of(c, li))];
-    });
-    uint64_t sum = 0;
-    for (size_t p = 0; p < kParts; ++p) {
-      off[p] = sum;
-      for (size_t c = 0; c < nc; ++c) {
-        const uint64_t v = cnt[c * kParts + p];
-        cnt[c * kParts + p] = sum;
-        sum += v;
-      }
-    }
-    off[kParts] = sum;
-    parallel_for(nc, hw, [&](size_t c) {
-      uint64_t* k = &cnt[c * kParts];
-      for (size_t li = 0; li < lines[c].size(); ++li)
-        loc[k[part_of(hash_of(c, li))]++] = ((uint64_t)c << 32) | li;
-    });
-  };
-  // open-addressing slots: {hash tag, global line index + 1 (0: empty)}; the
-  // partition took the hash's top bits, the slot index takes its low ones
-  struct Slot {
-    uint32_t tag, i1;
-  };
-  auto tag_of = [](uint64_t h) { return (uint32_t)(h >> 24); };
-  auto table_cap = [](uint64_t count) {
-    size_t cap = 16;
-    while (3 * cap < 4 * count) cap <<= 1;  // load <= 3/4
-    return cap;
-  };
-  // 1. renamings.  A line's ID S is taken iff S became a final key at an
-  // earlier line: t_S = min(S's first line, the first line whose generated
-  // name is S).  A generated name is longer than its ID, so the distinct IDs
-  // are settled in order of length: for each, its lines in file order (the
-  // first one keeps S when t_S is that line; every later one, and all of them
-  // when a shorter ID generated S first, take the next renaming), and each
-  // generated name that is some line's ID lowers that ID's t.  Where a
-  // generated name lands on a final key already made (the reference's
-  // unchecked overwrite), step 2 finds two equal final keys.
-  // (a) distinct IDs per partition, each line's ID number
-  scatter([&](size_t c, size_t li) { return lines[c][li].h_id; });
-  std::vector<uint32_t> lsid(n);             // per scattered position: local ID number
-  std::vector<uint64_t> nd(kParts + 1, 0);   // distinct IDs per partition, then prefix
-  std::vector<std::vector<Slot>> ids_tab(kParts);  // ID string -> global ID number + 1
-  parallel_for(kParts, hw, [&](size_t p) {
-    const size_t cap = table_cap(off[p + 1] - off[p]);
-    std::vector<Slot>& tab = ids_tab[p];
-    tab.assign(cap, Slot{0, 0});
-    std::vector<uint64_t> rep_loc;  // local ID -> its first line's locator
-    for (uint64_t q = off[p]; q < off[p + 1]; ++q) {
-      const GffLine& L = line_at(loc[q]);
-      const uint32_t tg = tag_of(L.h_id);
-      size_t s = L.h_id & (cap - 1);
-      while (tab[s].i1 && (tab[s].tag != tg || line_at(rep_loc[tab[s].i1 - 1]).id != L.id))
-        s = (s + 1) & (cap - 1);
-      if (!tab[s].i1) {
-        rep_loc.push_back(loc[q]);
-        tab[s] = Slot{tg, (uint32_t)rep_loc.size()};
-      }
-      lsid[q] = tab[s].i1 - 1;
-    }
-    nd[p + 1] = rep_loc.size();
-  });
-  for (size_t p = 0; p < kParts; ++p) nd[p + 1] += nd[p];
-  lap("ids_table");
-  const uint64_t nids = nd[kParts];
-  // (b) per ID: its lines in file order (CSR), first line, length
-  std::vector<uint64_t> occ_off(nids + 1, 0);
-  std::vector<uint32_t> occ(n), len_of(nids), first_line(nids);
-  std::vector<std::atomic<uint32_t>> gen_t(nids);
-  std::atomic<uint32_t> max_len{0};
-  parallel_for(kParts, hw, [&](size_t p) {
-    const uint64_t g0 = nd[p], nl = nd[p + 1] - nd[p];
-    std::vector<uint64_t> w(nl, 0);
-    for (uint64_t q = off[p]; q < off[p + 1]; ++q) ++w[lsid[q]];
-    uint64_t sum = off[p];  // the partition's lines are loc[off[p] .. off[p + 1])
-    for (uint64_t k = 0; k < nl; ++k) {
-      occ_off[g0 + k] = sum;
-      sum += w[k];
-      w[k] = occ_off[g0 + k];
-    }
-    uint32_t ml = 0;
-    for (uint64_t q = off[p]; q < off[p + 1]; ++q) {
-      const uint64_t g = g0 + lsid[q];
-      occ[w[lsid[q]]++] = (uint32_t)gidx(loc[q]);
-      const uint32_t ln = (uint32_t)std::min<size_t>(line_at(loc[q]).id.size(), 0xFFFFFFFFu);
-      len_of[g] = ln;
-      ml = std::max(ml, ln);
-    }
-    for (uint64_t k = 0; k < nl; ++k) {
-      first_line[g0 + k] = occ[occ_off[g0 + k]];
-      gen_t[g0 + k].store(~0u, std::memory_order_relaxed);
-    }
-    for (Slot& sl : ids_tab[p])
-      if (sl.i1) sl.i1 += (uint32_t)g0;  // local -> global ID number + 1
-    uint32_t cur = max_len.load();
-    while (ml > cur && !max_len.compare_exchange_weak(cur, ml)) {
-    }
-  });
-  occ_off[nids] = n;
-  lap("id_lines");
-  std::vector<uint32_t>().swap(lsid);
-  if (max_len.load() > 4096) return false;  // absurd IDs: the serial pass
-  // (c) IDs bucketed by length, settled level by level
-  std::vector<uint64_t> lvl_off(max_len.load() + 2, 0);
-  std::vector<uint32_t> by_len(nids);
-  for (uint64_t g = 0; g < nids; ++g) ++lvl_off[len_of[g] + 1];
-  for (size_t k = 1; k < lvl_off.size(); ++k) lvl_off[k] += lvl_off[k - 1];
-  {
-    std::vector<uint64_t> w(lvl_off.begin(), lvl_off.end() - 1);
-    for (uint64_t g = 0; g < nids; ++g) by_len[w[len_of[g]]++] = (uint32_t)g;
-  }
-  auto find_id = [&](sv s, uint64_t h) -> int64_t {  // global ID number of a string, or -1
-    const std::vector<Slot>& tab = ids_tab[part_of(h)];
-    const size_t cap = tab.size();
-    const uint32_t tg = tag_of(h);
-    for (size_t q = h & (cap - 1); tab[q].i1; q = (q + 1) & (cap - 1))
-      if (tab[q].tag == tg && len_of[tab[q].i1 - 1] == s.size() &&
-          line_at(locate(first_line[tab[q].i1 - 1])).id == s)
-        return tab[q].i1 - 1;
-    return -1;
-  };
-  for (size_t lv = 0; lv + 1 < lvl_off.size(); ++lv) {
-    const uint64_t a0 = lvl_off[lv], a1 = lvl_off[lv + 1];
-    if (a0 == a1) continue;
-    const size_t tasks = (size_t)std::min<uint64_t>(4 * hw, a1 - a0);
-    parallel_for(tasks, hw, [&](size_t k) {
-      std::string nm;
-      for (uint64_t x = a0 + (a1 - a0) * k / tasks; x < a0 + (a1 - a0) * (k + 1) / tasks; ++x) {
-        const uint32_t g = by_len[x];
-        const uint32_t t = std::min(first_line[g], gen_t[g].load(std::memory_order_relaxed));
-        uint32_t j = 0;
-        for (uint64_t o = occ_off[g]; o < occ_off[g + 1]; ++o) {
-          const uint32_t i = occ[o];
-          const GffLine& L = line_at(locate(i));
-          if (i == t) {  // its first line, before any generated copy: keeps the ID
-            rep[i] = 0;
-            fkh[i] = L.h_id;
-            continue;
-          }
-          rep[i] = ++j;
-          dup_name(L.id, j, nm);
-          const uint64_t h = j == L.dup_run ? L.h_dup : hash_sv(nm);
-          fkh[i] = h;
-          const int64_t gg = find_id(nm, h);
-          if (gg >= 0) {  // the generated name is another ID: taken from line i on
-            std::atomic<uint32_t>& tm = gen_t[(size_t)gg];
-            uint32_t cur = tm.load(std::memory_order_relaxed);
-            while (i < cur && !tm.compare_exchange_weak(cur, i, std::memory_order_relaxed)) {
-            }
-          }
-        }
-      }
-    });
-  }
-  lap("renamings");
-  // 2. final keys distinct; the tables stay for the parent lookups
-  scatter([&](size_t c, size_t li) { return fkh[base[c] + li]; });
-  std::vector<std::vector<Slot>> keys(kParts);
-  std::atomic<bool> clash{false};
-  parallel_for(kParts, hw, [&](size_t p) {
-    const size_t cap = table_cap(off[p + 1] - off[p]);
-    std::vector<Slot>& tab = keys[p];
-    tab.assign(cap, Slot{0, 0});
-    std::string nm;
-    for (uint64_t q = off[p]; q < off[p + 1] && !clash.load(std::memory_order_relaxed); ++q) {
-      const uint64_t i = gidx(loc[q]);
-      const uint64_t h = fkh[i];
-      const uint32_t tg = tag_of(h);
-      size_t s = h & (cap - 1);
-      for (; tab[s].i1; s = (s + 1) & (cap - 1)) {
-        if (tab[s].tag != tg || fkh[tab[s].i1 - 1] != h) continue;
-        key_of(loc[q], nm);
-        if (key_is(locate(tab[s].i1 - 1), nm)) {
-          clash = true;
-          return;
-        }
-      }
-      tab[s] = Slot{tg, (uint32_t)(i + 1)};
-    }
-  });
-  lap("final_keys");
-  if (clash) return false;
-  // 3. parents: the earlier line whose final key the line names
-  std::vector<uint32_t> holder(n, ~0u);
-  parallel_for(nc, hw, [&](size_t c) {
-    sv last;
-    uint32_t last_j = ~0u;
-    for (size_t li = 0; li < lines[c].size(); ++li) {
-      const GffLine& L = lines[c][li];
-      if (!L.has_parent) continue;
-      const uint64_t i = base[c] + li;
-      if (last_j == ~0u || L.parent != last) {
-        const std::vector<Slot>& tab = keys[part_of(L.h_parent)];
-        const size_t cap = tab.size();
-        const uint32_t tg = tag_of(L.h_parent);
-        size_t s = L.h_parent & (cap - 1);
-        while (tab[s].i1 && (tab[s].tag != tg || fkh[tab[s].i1 - 1] != L.h_parent ||
-                             !key_is(locate(tab[s].i1 - 1), L.parent)))
-          s = (s + 1) & (cap - 1);
-        if (!tab[s].i1) throw Unsupported();  // no line holds it: orphan
-        last_j = tab[s].i1 - 1;
-        last = L.parent;
-      }
-      if (last_j >= i) throw Unsupported();  // held only by a later line: orphan here
-      holder[i] = last_j;
-    }
-  });
-  lap("parents");
-  std::vector<std::vector<Slot>>().swap(keys);
-  // 4. seqids, strands and tables in first-seen order (chunk by chunk)
-  std::vector<std::vector<uint32_t>> sq_of(nc), st_of(nc), ty_of(nc);
-  std::vector<std::vector<uint8_t>> ty_base(nc);
-  for (size_t c = 0; c < nc; ++c) {
-    const LineParser& P = *parsers[c];
-    for (sv x : P.seqids.strs) sq_of[c].push_back(M.seqids.intern(x));
-    for (sv x : P.strands.strs) st_of[c].push_back(M.strands.intern(x));
-    for (sv x : P.ftypes.strs) {
-      ty_of[c].push_back(M.table(x));
-      ty_base[c].push_back(x == "CDS" || x == "match_part" || x == "similarity" || x == "region");
-    }
-  }
-  lap("interning");
-  // per-table line counts, then every table's keys, feature i and ID i
-  const size_t nt = M.tables.size();
-  std::vector<uint64_t> tcnt(nc * nt, 0);
-  parallel_for(nc, hw, [&](size_t c) {
-    for (const GffLine& L : lines[c]) ++tcnt[c * nt + ty_of[c][L.ftype]];
-  });
-  for (size_t t = 0; t < nt; ++t) {
-    uint64_t sum = 0;
-    for (size_t c = 0; c < nc; ++c) {
-      const uint64_t v = tcnt[c * nt + t];
-      tcnt[c * nt + t] = sum;
-      sum += v;
-    }
-    M.tables[t].keys.resize(sum);
-  }
-  uint64_t key_bytes = 0;
-  std::vector<uint64_t> kb(nc + 1, 0);  // storage offset of each chunk's final keys
-  for (size_t c = 0; c < nc; ++c) {
-    for (size_t li = 0; li < lines[c].size(); ++li) {
-      const uint32_t j = rep[base[c] + li];
-      char b[16];
-      key_bytes += lines[c][li].id.size() + (j ? suffix(j, b).size() : 0);
-    }
-    kb[c + 1] = key_bytes;
-  }
-  char* store = new char[std::max<uint64_t>(key_bytes, 1)];
-  M.ids.chunks.emplace_back(store);
-  M.feats.resize(n);
-  M.id_types.resize(n);
-  M.first_table.resize(n);
-  M.first_feat.resize(n);
-  M.ids.strs.resize(n);
-  parallel_for(nc, hw, [&](size_t c) {
-    char* o = store + kb[c];
-    for (size_t li = 0; li < lines[c].size(); ++li) {
-      const GffLine& L = lines[c][li];
-      const uint64_t i = base[c] + li;
-      const uint32_t t = ty_of[c][L.ftype];
-      char b[16];
-      const sv x = rep[i] ? suffix(rep[i], b) : sv();
-      memcpy(o, L.id.data(), L.id.size());
-      if (!x.empty()) memcpy(o + L.id.size(), x.data(), x.size());
-      M.ids.strs[i] = sv(o, L.id.size() + x.size());
-      o += L.id.size() + x.size();
-      Feature& f = M.feats[i];
-      f.type = t;
-      f.seqid = sq_of[c][L.seqid];
-      f.lo = L.lo;
-      f.hi = L.hi;
-      f.strand = st_of[c][L.strand];
-      f.base = ty_base[c][L.ftype];
-      f.kids = ~0u;
-      M.id_types[i] = 1ull << t;
-      M.first_table[i] = (uint8_t)t;
-      M.first_feat[i] = (uint32_t)i;
-      M.tables[t].keys[tcnt[c * nt + t]++] = (uint32_t)i;
-    }
-  });
-  lap("fill");
-  // 5. child lists in file order
-  M.link_child.reserve(n);
-  M.link_next.reserve(n);
-  for (uint64_t i = 0; i < n; ++i) {
-    const uint32_t h = holder[i];
-    if (h == ~0u) continue;
-    Feature& hf = M.feats[h];
-    if (hf.base) throw Unsupported();  // BaseAnnotation has no child_list
-    M.add_child(hf, (uint32_t)i);
-  }
-  lap("children");
-  return true;
-}
-
 // read_gff in two passes: the per-line work (columns, tags, IDs, hashes) in
 // parallel over newline-aligned chunks of the text, then the model updates
 // (de-duplication, tables, parents) in file order.  Any diagnostic path
@@ -1143,17 +747,6 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
             (unsigned long long)n_chunks);
   uint64_t total = 0;
   for (auto& v : lines) total += v.size();
-  // without a GTF hierarchy the file-order pass runs on host threads unless
-  // two lines' final keys meet (ordered_parallel); MAGOT_GFF_SERIAL=1 forces
-  // the serial pass (A/B and tests)
-  const char* force_serial = std::getenv("MAGOT_GFF_SERIAL");
-  if (!hier && !(force_serial && force_serial[0] == '1') &&
-      ordered_parallel(M, lines, parsers, hw)) {
-    if (std::getenv("MAGOT_GFF_TIMING"))
-      fprintf(stderr, "[gffplan] ordered  %.3f s (parallel)\n",
-              std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
-    return;
-  }
   M.ids.reserve(total + 16);
   M.feats.reserve(total + 16);
   M.id_types.reserve(total + 16);

@@ -117,32 +117,6 @@ if has gffab; then
   AB_TIMING=1 timeout -k 10 600 bash scripts/gffplan_ab.sh run $OUT/gffab 4 > $OUT/gffab.log 2>&1 || { tail -20 $OUT/gffab.log; exit 1; }
   grep plan_s $OUT/gffab/gffplan_ab.txt
 fi
-if has gffpar; then
-  # the planner's file-order pass: threaded (default) against serial
-  # (MAGOT_GFF_SERIAL=1), alternating, on the C3 GFF3 written by the phase run
-  bash scripts/gffplan_ab.sh build scripts/ab_old/magot_amd/csrc/gffplan.cpp > $OUT/gffpar_build.log 2>&1 || { tail -20 $OUT/gffpar_build.log; exit 1; }
-  D=$(mktemp -d)
-  timeout -k 10 300 python - "$D" > $OUT/gffpar_gen.log 2>&1 <<'PY' || { tail -20 $OUT/gffpar_gen.log; exit 1; }
-import os, sys
-sys.path.insert(0, '.')
-from magot_amd import synth
-d = sys.argv[1]
-w = synth.make('C3', genome=False)
-open(os.path.join(d, 'ann.gff3'), 'w').write(w.gff3_text())
-open(os.path.join(d, 'ncbi.gff3'), 'w').write(w.gff3_text(ids='ncbi'))
-open(os.path.join(d, 'ctgs.txt'), 'w').write('\n'.join('%s %d' % (n, l) for n, l in zip(w.contig_names, w.contig_len)))
-PY
-  for f in ann ncbi; do
-    for i in 1 2 3 4; do
-      for v in par ser; do
-        ser=""; [ $v = ser ] && ser=1
-        MAGOT_GFF_TIMING=1 MAGOT_GFF_SERIAL=$ser timeout -k 10 120 scripts/gffplan_new.bin $D/$f.gff3 $D/ctgs.txt 1 2>&1 | sed "s/^/$f $v /" >> $OUT/gffpar.txt || exit 1
-      done
-    done
-  done
-  rm -rf $D
-  grep plan_s $OUT/gffpar.txt
-fi
 if has whole; then
   # the phase run (writes the C3 files and the reference out.fa; genome-order
   # plan as the CLI builds it), then three whole gff2fasta calls on those

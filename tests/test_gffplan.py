@@ -447,95 +447,3 @@ def test_two_step_abi_state_errors():
     assert L.magot_gff_lower(h, *args) == _lib.ERR_STATE      # lowered already
     L.magot_gffplan_destroy(h)
     assert L.magot_gff_lower(None, *args) == _lib.ERR_ARG
-
-
-# ---------------------------------------------------------------------------
-# read_gff's file-order pass on host threads (ordered_parallel in gffplan.cpp)
-# against the serial pass (MAGOT_GFF_SERIAL=1): same plans, and the serial
-# pass wherever two lines' final keys meet
-# ---------------------------------------------------------------------------
-
-def _both_paths(monkeypatch, fasta, gff, **kw):
-    monkeypatch.delenv('MAGOT_GFF_SERIAL', raising=False)
-    par = native_gff2fasta(fasta, gff, **kw)
-    monkeypatch.setenv('MAGOT_GFF_SERIAL', '1')
-    ser = native_gff2fasta(fasta, gff, **kw)
-    monkeypatch.delenv('MAGOT_GFF_SERIAL')
-    return par, ser
-
-
-@pytest.mark.parametrize('i', range(len(FUZZ_INPUTS)))
-def test_parallel_pass_equals_serial_on_fuzz(monkeypatch, i):
-    fasta, gff = FUZZ_INPUTS[i]
-    for kw in (dict(seq_type='protein', order='py2'), dict(seq_type='nucleotide', longest=True),
-               dict(seq_type='nucleotide', from_exons=True, order='insertion')):
-        par, ser = _both_paths(monkeypatch, fasta, gff, **kw)
-        assert par == ser, kw
-
-
-@pytest.mark.parametrize('chunks', [1, 3, 64])
-def test_parallel_pass_equals_serial_dup_heavy(monkeypatch, chunks):
-    monkeypatch.setenv('MAGOT_GFF_CHUNKS', str(chunks))
-    fasta = '>c1\n' + 'ACGTTGCAACGGAT' * 30 + '\n'
-    par, ser = _both_paths(monkeypatch, fasta, _dup_heavy_gff(), seq_type='protein', order='py2')
-    assert par is not None and par == ser
-
-
-# a literal ID2 after the renamed ID -> ID2: a cascade (ID2 is taken, so the
-# literal one becomes ID22), which the threaded pass settles itself
-_CASCADE_GFF = [
-    'c1\tx\tgene\t1\t90\t.\t+\t.\tID=g1', 'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=X;Parent=g1',
-    'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=X;Parent=g1', 'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=X2;Parent=g1',
-    'c1\tx\tmRNA\t1\t90\t.\t-\t.\tID=X2;Parent=g1', 'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=X22;Parent=g1',
-    'c1\tx\tCDS\t3\t30\t.\t+\t0\tID=c;Parent=X2', 'c1\tx\tCDS\t40\t60\t.\t+\t0\tID=c;Parent=X',
-    'c1\tx\tCDS\t20\t45\t.\t-\t0\tID=d;Parent=X22', 'c1\tx\tCDS\t50\t70\t.\t+\t0\tID=e;Parent=X2-3']
-
-
-def test_parallel_pass_cascade(monkeypatch, capfd):
-    fasta = '>c1\n' + 'ACGTTGCAACGGATCCATG' * 6 + '\n'
-    gff = '\n'.join(_CASCADE_GFF) + '\n'
-    monkeypatch.setenv('MAGOT_GFF_TIMING', '1')
-    par, ser = _both_paths(monkeypatch, fasta, gff, seq_type='protein', order='insertion')
-    assert '(parallel)' in capfd.readouterr().err
-    want, diag = _oracle_or_diag(fasta, gff, seq_type='protein', order='insertion')
-    assert not diag and par == ser == want
-
-
-_CLASH_GFFS = [
-    # the literal ID2 first, then ID twice: the rename overwrites ID2 unchecked
-    ['c1\tx\tgene\t1\t90\t.\t+\t.\tID=g1', 'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=X2;Parent=g1',
-     'c1\tx\tCDS\t3\t30\t.\t+\t0\tID=c;Parent=X2', 'c1\tx\tmRNA\t1\t90\t.\t-\t.\tID=X;Parent=g1',
-     'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=X;Parent=g1', 'c1\tx\tCDS\t40\t60\t.\t-\t0\tID=d;Parent=X'],
-    # two bases whose renamings meet: B-1's first (B-12) and B's eleventh (B-12)
-    ['c1\tx\tgene\t1\t90\t.\t+\t.\tID=g1', 'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=B-1;Parent=g1',
-     'c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=B-1;Parent=g1'] +
-    ['c1\tx\tmRNA\t1\t90\t.\t+\t.\tID=B;Parent=g1'] * 12 +
-    ['c1\tx\tCDS\t3\t30\t.\t+\t0\tID=c;Parent=B-12', 'c1\tx\tCDS\t5\t50\t.\t+\t0\tID=c;Parent=B'],
-]
-
-
-@pytest.mark.parametrize('k', range(len(_CLASH_GFFS)))
-def test_parallel_pass_clash_runs_serial(monkeypatch, capfd, k):
-    fasta = '>c1\n' + 'ACGTTGCAACGGATCCATG' * 6 + '\n'
-    gff = '\n'.join(_CLASH_GFFS[k]) + '\n'
-    monkeypatch.setenv('MAGOT_GFF_TIMING', '1')
-    par, ser = _both_paths(monkeypatch, fasta, gff, seq_type='protein', order='insertion')
-    err = capfd.readouterr().err
-    assert '(parallel)' not in err  # the meeting final keys sent it to the serial pass
-    want, diag = _oracle_or_diag(fasta, gff, seq_type='protein', order='insertion')
-    assert par == ser
-    assert par is None if diag else par == want
-
-
-def test_parallel_pass_is_taken(monkeypatch, capfd):
-    """On a GFF3 without meeting final keys the threaded pass runs (and gives
-    the oracle's text); on a GTF (hierarchy) the serial pass does."""
-    w = synth.make('small', seed=8, genome_bases=200_000, n_tx=150, iupac_rate=1e-3)
-    fasta = w.fasta_text()
-    monkeypatch.setenv('MAGOT_GFF_TIMING', '1')
-    got = native_gff2fasta(fasta, w.gff3_text(), 'protein', 'py2')
-    assert '(parallel)' in capfd.readouterr().err
-    assert got == mo.gff2fasta(fasta, w.gff3_text(), seq_type='protein', order='py2')
-    got = native_gff2fasta(fasta, w.gtf_text(), 'protein', 'py2')
-    assert '(parallel)' not in capfd.readouterr().err
-    assert got == mo.gff2fasta(fasta, w.gtf_text(), seq_type='protein', order='py2')
