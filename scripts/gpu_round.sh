@@ -129,6 +129,16 @@ if has whole; then
   done
   rm -rf /tmp/magot_e2e
 fi
+if has wholenuc; then
+  # the same for seq_type=nucleotide (606 MB of text)
+  MAGOT_GFF_TIMING=1 timeout -k 10 900 python scripts/e2e_cli.py --config C3 --seq-type nucleotide --layout genome > $OUT/e2e_nucleotide.json 2> $OUT/e2e_nuc.err || { tail -20 $OUT/e2e_nuc.err; exit 1; }
+  cat $OUT/e2e_nucleotide.json
+  for i in 1 2 3; do
+    timeout -k 10 300 python scripts/e2e_cli.py --config C3 --seq-type nucleotide --whole > $OUT/e2e_whole_nuc$i.json 2> $OUT/e2e_whole_nuc$i.err || { tail -20 $OUT/e2e_whole_nuc$i.err; exit 1; }
+    cat $OUT/e2e_whole_nuc$i.json
+  done
+  rm -rf /tmp/magot_e2e
+fi
 if has multi; then
   # two ranks launched by bench itself, sharing the one card over gloo (the
   # C4 orchestration; the driver's 8-GPU node runs it over RCCL)
