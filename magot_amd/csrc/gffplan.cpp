@@ -528,6 +528,7 @@ struct LineParser {
   sv prev_id;
   uint32_t prev_run = 0;
   std::string dup;
+  std::vector<uint64_t> type_lines;  // accepted lines per local type code
 
   // false: the line is skipped; throws Unsupported on a diagnostic path
   bool parse(const char* raw, uint64_t rl, GffLine& L, GffHier& H) {
@@ -561,6 +562,8 @@ struct LineParser {
     L.hi = hi;
     L.seqid = seqids.code(cols[0]);
     L.ftype = ftypes.code(ftype);
+    if (L.ftype >= type_lines.size()) type_lines.resize(L.ftype + 1, 0);
+    ++type_lines[L.ftype];
     L.strand = strands.code(cols[6]);
     tags.kv.clear();
     size_t b = 0;
@@ -758,11 +761,30 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
   // model updates in file order
   std::vector<uint32_t> renamed;  // per ID: 0, or the last suffix used
   renamed.reserve(total + 16);
+  // the hierarchy's tables, then every line type's table in first-seen order
+  // (chunk by chunk: what the pass below would create at each type's first
+  // line), so the tables' key lists can be reserved for their lines
+  std::vector<uint32_t> hier_table;
+  for (const std::string& hk : F.hierarchy)
+    hier_table.push_back(M.table(sv(hk).substr(0, hk.find('_'))));
+  {
+    std::vector<uint64_t> want(M.tables.size(), 0);
+    for (uint64_t c = 0; c < n_chunks; ++c) {
+      const LineParser& P = *parsers[c];
+      for (size_t k = 0; k < P.ftypes.strs.size(); ++k) {
+        const uint32_t t = M.table(P.ftypes.strs[k]);
+        if (t >= want.size()) want.resize(t + 1, 0);
+        want[t] += k < P.type_lines.size() ? P.type_lines[k] : 0;
+      }
+    }
+    for (size_t t = 0; t < want.size(); ++t) M.tables[t].keys.reserve(want[t] + 16);
+  }
   {
     // the ordered pass below writes these in growing order; their pages are
     // mapped here, on every host thread at once (C3: ~0.5 GB that the pass
     // would otherwise fault in one page at a time)
     Prefault pf;
+    for (const Table& t : M.tables) pf.add(t.keys.data(), t.keys.capacity() * 4);
     pf.add(&M.ids.slots[0], M.ids.slots.size() * 8);
     pf.add(M.ids.strs.data(), M.ids.strs.capacity() * sizeof(sv));
     pf.add(M.feats.data(), M.feats.capacity() * sizeof(Feature));
@@ -779,9 +801,6 @@ void read_gff(Model& M, const char* text, uint64_t n, bool from_exons) {
               pf.bytes() >> 20);
   }
   std::string nid;
-  std::vector<uint32_t> hier_table;
-  for (const std::string& hk : F.hierarchy)
-    hier_table.push_back(M.table(sv(hk).substr(0, hk.find('_'))));
   std::vector<uint32_t> sq_of, st_of, ty_of;  // chunk code -> model index
   std::vector<uint8_t> ty_base;
   constexpr size_t kAhead = 16;
