@@ -42,7 +42,7 @@ struct Feature {
   int64_t lo = 0, hi = 0;
   uint32_t strand = 0;  // index into Model::strands
   bool base = false;
-  uint32_t kids = ~0u;  // its child list (Model::kid_lists), ~0u: none yet
+  uint32_t kids = ~0u;  // its child list (Model::kid_head), ~0u: none yet
 };
 
 struct Table {
